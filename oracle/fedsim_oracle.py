@@ -1,0 +1,300 @@
+"""CPU restatement of the reference's federated round -- TEST INFRASTRUCTURE ONLY.
+
+This module is the *oracle* (checker) for the MI355X HIP path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it,
+and only as the checker / the CPU baseline -- never as the product path.  The
+product (``fedamw_amd``) has no CPU fallback and never imports this file.
+
+What it restates (numpy float32, closed-form gradients, one client at a time):
+
+  * ``lr_schedule``      -- ``update_learning_rate``        tools.py:43-61  (compounding)
+  * ``mlp_init``         -- ``MLP.__init__``                tools.py:34-40  (Kaiming draw then Xavier, Q12)
+  * ``pass_order``       -- one ``DataLoader(shuffle=True)`` pass's RNG use (Q11)
+  * ``train_client``     -- ``train_loop``                  tools.py:177-215 (unsquared prox/ridge, Q2/Q5)
+  * ``test_eval``        -- ``test_loop`` + ``comp_accuracy`` + ``Meter``  tools.py:218-237, 82-166 (Q13)
+  * ``aggregate``        -- the inline left fold            tools.py:345-350
+  * ``mixture_solve``    -- FedAMW's p-SGD                  tools.py:441-453 (Q6, Q7)
+  * ``FedAvg/FedProx/FedAMW`` -- round drivers              tools.py:329-380, 413-463
+
+The RNG stream is torch's own CPU generator (the generator the reference draws
+from), used through the same calls the reference's DataLoader makes, so seeds
+line up draw-for-draw.  ``clients='sequential'`` is the reference semantics
+(client i starts from client i-1's weights); ``clients='parallel'``
+starts every client from the round's global model (the harness-level variant
+the golden generator builds by calling the reference's own ``train_loop`` on a
+deep copy per client).
+
+Parity pinning: this oracle is checked against the golden fixtures in
+``tests/golden/`` that ``tests/golden/make_golden.py`` produced by importing the
+unmodified reference ``functions/tools.py`` in the build container
+(``tests/test_oracle_golden.py``).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+F32 = np.float32
+
+
+# --------------------------------------------------------------------------- #
+# small pieces
+# --------------------------------------------------------------------------- #
+def lr_schedule(t: int, lr: float, R: int) -> float:
+    """tools.py:43-61 -- returns the *new* lr; callers rebind it (tools.py:338)."""
+    if t == int(R / 2):
+        return lr / 10
+    if t == int(R * 0.75):
+        return lr / 100
+    return lr
+
+
+def mlp_init(D: int, C: int) -> np.ndarray:
+    """tools.py:34-40: nn.Linear(D, C, bias=False) default init, then xavier_uniform_.
+
+    Consumes the global torch RNG exactly like ``MLP(D, C)`` (C*D uniforms for the
+    discarded Kaiming draw, then C*D for Xavier).
+    """
+    w = torch.empty(C, D)
+    torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    torch.nn.init.xavier_uniform_(w)
+    return w.numpy().astype(F32)
+
+
+def pass_order(n: int, shuffle: bool = True) -> np.ndarray:
+    """RNG use of one pass over ``DataLoader(TensorDataset, batch_size, shuffle)``.
+
+    iter() draws the worker base seed (1 int64); RandomSampler draws its seed
+    (1 int64) and runs randperm(n) on a private generator.
+    tools.py:178-179, 190 (train), 219-220, 229 (test), exp.py:99 (valid).
+    """
+    torch.empty((), dtype=torch.int64).random_()
+    if not shuffle:
+        return np.arange(n)
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g).numpy()
+
+
+def _log_softmax(z: np.ndarray) -> np.ndarray:
+    m = z.max(axis=1, keepdims=True)
+    s = np.exp(z - m).sum(axis=1, keepdims=True, dtype=F32)
+    return (z - m - np.log(s)).astype(F32)
+
+
+# --------------------------------------------------------------------------- #
+# train_loop / test_loop
+# --------------------------------------------------------------------------- #
+def train_client(X, y, W, lr, epoch, batch_size, prox, mu, reg, lam):
+    """tools.py:177-215.  Returns (W_new, last-epoch mean loss).
+
+    Per batch (size |b| <= batch_size, last one short):
+      z = X_b W^T ; L = CE_mean(z, y) [+ mu*||W-W_a||_F] [+ lam*||W||_F]   (tools.py:194-209)
+      grad = (softmax(z) - onehot)^T X_b / |b| [+ mu (W-W_a)/||W-W_a||] [+ lam W/||W||]
+      (a zero norm contributes a zero gradient, as torch's norm backward does -- Q2)
+      W -= lr * grad                                                         (tools.py:210-211)
+    The reported loss is the |b|-weighted mean over the LAST epoch (Meter reset
+    per epoch, tools.py:187-189, 212, 215).
+    """
+    X = np.asarray(X, dtype=F32)
+    y = np.asarray(y, dtype=np.int64)
+    W = np.array(W, dtype=F32, copy=True)
+    Wa = W.copy()                                  # global_model = deepcopy(model)  tools.py:180
+    lr32, mu32, lam32 = F32(lr), F32(mu), F32(lam)
+    n = len(y)
+    avg = 0.0
+    for _ in range(epoch):
+        order = pass_order(n)
+        s, cnt = 0.0, 0
+        for b0 in range(0, n, batch_size):
+            idx = order[b0:b0 + batch_size]
+            xb, yb = X[idx], y[idx]
+            bsz = len(idx)
+            z = xb @ W.T
+            logp = _log_softmax(z)
+            ce = F32(-logp[np.arange(bsz), yb].mean(dtype=F32))
+            g = np.exp(logp).astype(F32)
+            g[np.arange(bsz), yb] -= F32(1.0)
+            g /= F32(bsz)
+            grad = (g.T @ xb).astype(F32)
+            loss = ce
+            if prox:
+                dw = W - Wa
+                pn = F32(np.sqrt(np.sum(dw * dw, dtype=F32)))
+                loss = F32(loss + mu32 * pn)
+                if pn > 0:
+                    grad = grad + mu32 * (dw / pn)
+            if reg:
+                wn = F32(np.sqrt(np.sum(W * W, dtype=F32)))
+                loss = F32(loss + lam32 * wn)
+                if wn > 0:
+                    grad = grad + lam32 * (W / wn)
+            W = (W - lr32 * grad.astype(F32)).astype(F32)
+            s += float(loss) * bsz
+            cnt += bsz
+        avg = s / cnt if cnt else 0.0
+    return W, avg
+
+
+def test_eval(X, y, W, batch_size=32):
+    """tools.py:218-237 (+ comp_accuracy tools.py:82-96, Meter tools.py:99-148).
+
+    Shuffled batches of ``batch_size``; loss = sum_b CE_mean_b*|b| / n,
+    acc = sum_b (100*correct_b/|b|)*|b| / n  (percent, Q13).
+    """
+    X = np.asarray(X, dtype=F32)
+    y = np.asarray(y, dtype=np.int64)
+    n = len(y)
+    order = pass_order(n)
+    ls, acs, cnt = 0.0, 0.0, 0
+    for b0 in range(0, n, batch_size):
+        idx = order[b0:b0 + batch_size]
+        xb, yb = X[idx], y[idx]
+        bsz = len(idx)
+        z = xb @ W.T
+        logp = _log_softmax(z)
+        ce = F32(-logp[np.arange(bsz), yb].mean(dtype=F32))
+        correct = F32((z.argmax(axis=1) == yb).sum())
+        acc = F32(correct * F32(100.0 / bsz))
+        ls += float(ce) * bsz
+        acs += float(acc) * bsz
+        cnt += bsz
+    return ls / cnt, acs / cnt
+
+
+def aggregate(Ws, p):
+    """tools.py:345-350: global = p0*W0 + p1*W1 + ... as a float32 left fold,
+    every product and every sum rounded separately."""
+    p = np.asarray(p, dtype=F32)
+    acc = (Ws[0] * p[0]).astype(F32)
+    for j in range(1, len(Ws)):
+        acc = (acc + (p[j] * Ws[j]).astype(F32)).astype(F32)
+    return acc
+
+
+def mixture_solve(Ws, Xv, yv, p, buf, lr_p, epochs, batch_size=16, momentum=0.9):
+    """tools.py:441-453: ``epochs`` passes of SGD(momentum) on p over the pooled
+    validation set.  out[b,c] = sum_n p_n Z[n,c,b], Z[n,c,b] = W_n[c,:].x_b (Q7);
+    buf = grad on the very first step (buf is None), else 0.9*buf + grad;
+    p -= lr_p*buf.  ``buf`` persists across rounds (optimizer built once, tools.py:423).
+    Returns (p, buf).
+    """
+    Xv = np.asarray(Xv, dtype=F32)
+    yv = np.asarray(yv, dtype=np.int64)
+    W3 = np.stack(Ws, axis=0).astype(F32)          # [N, C, D]
+    Z = np.einsum('ncd,vd->ncv', W3, Xv, optimize=True).astype(F32)   # [N, C, n_v]
+    p = np.array(p, dtype=F32, copy=True)
+    lr32, mom32 = F32(lr_p), F32(momentum)
+    nv = len(yv)
+    for _ in range(epochs):
+        order = pass_order(nv)
+        for b0 in range(0, nv, batch_size):
+            idx = order[b0:b0 + batch_size]
+            bsz = len(idx)
+            zb = Z[:, :, idx]                       # [N, C, b]
+            out = np.einsum('ncb,n->bc', zb, p).astype(F32)
+            logp = _log_softmax(out)
+            g = np.exp(logp).astype(F32)
+            g[np.arange(bsz), yv[idx]] -= F32(1.0)
+            g /= F32(bsz)
+            gp = np.einsum('bc,ncb->n', g, zb).astype(F32)
+            buf = gp.copy() if buf is None else (mom32 * buf + gp).astype(F32)
+            p = (p - lr32 * buf).astype(F32)
+    return p, buf
+
+
+# --------------------------------------------------------------------------- #
+# round drivers
+# --------------------------------------------------------------------------- #
+def _as_np_list(xs, dtype):
+    return [np.asarray(x.numpy() if isinstance(x, torch.Tensor) else x, dtype=dtype) for x in xs]
+
+
+def _weights(ys):
+    num = np.array([len(y) for y in ys])
+    return (num / sum(num)).astype(F32)
+
+
+def _local_round(Xs, ys, Wg, lr, epoch, batch_size, prox, mu, reg, lam, clients):
+    Ws, losses = [], []
+    W = Wg
+    for X, y in zip(Xs, ys):
+        start = Wg if clients == 'parallel' else W
+        W, l = train_client(X, y, start, lr, epoch, batch_size, prox, mu, reg, lam)
+        Ws.append(W)
+        losses.append(l)
+    return Ws, losses
+
+
+def FedAvg(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200,
+           lr=0.01, epoch=2, batch_size=32, prox=False, mu=0.1, lambda_reg_if=False,
+           lambda_reg=0.01, round=100, clients='sequential'):
+    """tools.py:329-353 (FedProx = same with prox=True, tools.py:356-380).
+
+    Returns (train_loss[R], test_loss[R], test_acc[R], trace) with
+    trace = {'W': [R, C, D] global weights after each round}.
+    """
+    Xs = _as_np_list(X_train, F32)
+    ys = _as_np_list(y_train, np.int64)
+    Xt = np.asarray(X_test, dtype=F32)
+    yt = np.asarray(y_test, dtype=np.int64)
+    Wg = mlp_init(D, num_classes)
+    p = _weights(ys)
+    tr = np.zeros(round, F32)
+    tl = np.zeros(round, F32)
+    ta = np.zeros(round, F32)
+    Wtr = []
+    for t in range(round):
+        lr = lr_schedule(t, lr, round)
+        Ws, losses = _local_round(Xs, ys, Wg, lr, epoch, batch_size, prox, mu,
+                                  lambda_reg_if, lambda_reg, clients)
+        tr[t] = np.sum(p * np.asarray(losses, dtype=F32), dtype=F32)
+        Wg = aggregate(Ws, p)
+        Wtr.append(Wg.copy())
+        tl[t], ta[t] = test_eval(Xt, yt, Wg, batch_size)
+    return tr, tl, ta, {'W': np.stack(Wtr)}
+
+
+def FedProx(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200,
+            lr=0.01, epoch=2, batch_size=32, prox=True, mu=0.1, lambda_reg_if=False,
+            lambda_reg=0.01, round=100, clients='sequential'):
+    """tools.py:356-380 -- FedAvg with prox defaulting to True."""
+    return FedAvg(X_train, y_train, X_test, y_test, type, num_classes, D, lr, epoch, batch_size,
+                  prox, mu, lambda_reg_if, lambda_reg, round, clients=clients)
+
+
+def FedAMW(X_train, y_train, X_test, y_test, X_val, y_val, type='classification', num_classes=10,
+           D=200, lr=0.01, epoch=2, batch_size=32, prox=False, mu=0.1, lambda_reg_if=True,
+           lambda_reg=0.01, round=100, lr_p=5e-5, clients='sequential', val_batch_size=16):
+    """tools.py:413-463.  The validation set is passed as arrays (the reference
+    takes a DataLoader with batch 16 and shuffle=True, exp.py:98-99).
+
+    Returns (train_loss, test_loss, test_acc, trace) with trace = {'W': [R,C,D], 'p': [R,N]}.
+    """
+    Xs = _as_np_list(X_train, F32)
+    ys = _as_np_list(y_train, np.int64)
+    Xt = np.asarray(X_test, dtype=F32)
+    yt = np.asarray(y_test, dtype=np.int64)
+    Xv = np.asarray(X_val, dtype=F32)
+    yv = np.asarray(y_val, dtype=np.int64)
+    Wg = mlp_init(D, num_classes)
+    p = _weights(ys)
+    buf = None
+    tr = np.zeros(round, F32)
+    tl = np.zeros(round, F32)
+    ta = np.zeros(round, F32)
+    Wtr, ptr = [], []
+    for t in range(round):
+        lr = lr_schedule(t, lr, round)
+        Ws, losses = _local_round(Xs, ys, Wg, lr, epoch, batch_size, prox, mu,
+                                  lambda_reg_if, lambda_reg, clients)
+        tr[t] = np.sum(p * np.asarray(losses, dtype=F32), dtype=F32)     # tools.py:434 (old p)
+        p, buf = mixture_solve(Ws, Xv, yv, p, buf, lr_p, round, val_batch_size)
+        Wg = aggregate(Ws, p)
+        Wtr.append(Wg.copy())
+        ptr.append(p.copy())
+        tl[t], ta[t] = test_eval(Xt, yt, Wg, batch_size)
+    return tr, tl, ta, {'W': np.stack(Wtr), 'p': np.stack(ptr)}

@@ -1,0 +1,257 @@
+"""Golden-vector generator: runs the UNMODIFIED reference ``functions/tools.py``.
+
+Run only in the build container (``/root/reference`` does not exist on the GPU
+box):  ``python tests/golden/make_golden.py``.  Writes small ``.npz`` fixtures
+next to this script: inputs (seeded synthetic RFF features), the seed, and the
+reference's outputs -- ``train_loss``, ``test_loss``, ``test_acc`` (the three
+return tensors) plus the global weight matrix after every round (captured by
+wrapping ``test_loop``, which every round driver calls right after
+``model.load_state_dict(global_weights)``) and, for FedAMW, the learned mixture
+weights ``p`` after every round.
+
+Two client modes are recorded:
+  * ``seq``: the reference drivers ``FedAvg`` / ``FedProx`` / ``FedAMW`` called
+    positionally, exactly as ``exp.py:116-127`` calls them (clients chained, Q1).
+  * ``par``: a harness-level variant in which every client starts from a
+    ``copy.deepcopy`` of the round's global model; it calls the reference's own
+    ``MLP``, ``update_learning_rate``, ``train_loop`` and ``test_loop``; only the
+    per-client model copy differs.  For FedAMW the p-SGD is driven here with the
+    same torch ops as tools.py:441-453.
+
+Unit fixtures for one ``train_loop`` call and one ``test_loop`` call are also
+written (``unit_train_*.npz``, ``unit_test.npz``).
+
+The reference's source never leaves this container; only these fixtures do.
+"""
+import contextlib
+import copy
+import io
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = '/root/reference'
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REF)
+import functions.tools as T  # noqa: E402  (the reference, unmodified)
+
+_trace = {'W': [], 'p': []}
+_orig_test_loop = T.test_loop
+
+
+def _recording_test_loop(X_test, y_test, type='classification', model=None, batch_size=32):
+    _trace['W'].append(model.classifier.weight.detach().clone().numpy())
+    caller = sys._getframe(1)
+    if 'p' in caller.f_locals and caller.f_code.co_name in ('FedAMW', '_fedamw_par'):
+        _trace['p'].append(caller.f_locals['p'].detach().clone().numpy())
+    return _orig_test_loop(X_test, y_test, type, model, batch_size)
+
+
+T.test_loop = _recording_test_loop
+
+
+def synth(seed, sizes, n_test, n_raw, D, C, sigma=0.5, alpha=0.3, val_frac=0.0):
+    """Seeded synthetic RFF features: raw binary X (a9a-like), phi = D^-1/2 cos(XW+b),
+    labels from a random teacher, Dirichlet(alpha) label skew across clients."""
+    rs = np.random.RandomState(seed)
+    total = int(sum(sizes)) * 3 + n_test
+    Xraw = (rs.rand(total, n_raw) < 0.3).astype(np.float32)
+    Wr = rs.normal(0, sigma, size=(n_raw, D)).astype(np.float32)
+    br = rs.uniform(0, 2 * np.pi, size=(1, D)).astype(np.float32)
+    phi = (np.cos(Xraw @ Wr + br) / np.sqrt(D)).astype(np.float32)
+    teacher = rs.normal(size=(D, C)).astype(np.float32)
+    y = np.argmax(phi @ teacher + 0.3 * rs.normal(size=(total, C)) / np.sqrt(D), axis=1)
+    test_idx = np.arange(total - n_test, total)
+    pool = np.arange(total - n_test)
+    by_class = [list(rs.permutation(pool[y[pool] == c])) for c in range(C)]
+    Xs, ys, Xv, yv = [], [], [], []
+    for n in sizes:
+        mix = rs.dirichlet(np.repeat(alpha, C))
+        idx = []
+        while len(idx) < n:
+            c = int(rs.choice(C, p=mix))
+            if not by_class[c]:
+                c = max(range(C), key=lambda k: len(by_class[k]))
+            idx.append(by_class[c].pop())
+        idx = np.array(idx)
+        nv = int(n * val_frac)
+        if nv:
+            Xv.append(phi[idx[:nv]])
+            yv.append(y[idx[:nv]])
+        Xs.append(phi[idx[nv:]])
+        ys.append(y[idx[nv:]])
+    out = dict(X_test=phi[test_idx], y_test=y[test_idx].astype(np.int64))
+    out['X_train'] = np.concatenate(Xs)
+    out['y_train'] = np.concatenate(ys).astype(np.int64)
+    out['sizes'] = np.array([len(v) for v in ys], dtype=np.int64)
+    if val_frac:
+        out['X_val'] = np.concatenate(Xv)
+        out['y_val'] = np.concatenate(yv).astype(np.int64)
+    return out
+
+
+def _split(d):
+    off = np.concatenate([[0], np.cumsum(d['sizes'])])
+    Xs = [torch.from_numpy(d['X_train'][off[i]:off[i + 1]].copy()) for i in range(len(d['sizes']))]
+    ys = [torch.from_numpy(d['y_train'][off[i]:off[i + 1]].copy()) for i in range(len(d['sizes']))]
+    return Xs, ys, torch.from_numpy(d['X_test']), torch.from_numpy(d['y_test'])
+
+
+def _fed_par(X_train, y_train, X_test, y_test, type, num_classes, D, lr, epoch, batch_size,
+             prox, mu, lambda_reg_if, lambda_reg, round):
+    """Harness: FedAvg/FedProx round loop with a fresh copy of the global model per client."""
+    model = T.MLP(D, num_classes).to(T.device)
+    n = np.array([len(y) for y in y_train])
+    p = torch.tensor(n / sum(n), dtype=torch.float32)
+    out = [torch.zeros(round) for _ in range(3)]
+    for t in range(round):
+        lr = T.update_learning_rate(t, lr, round)
+        Ws, losses = [], []
+        for i in range(len(y_train)):
+            local = copy.deepcopy(model)
+            w, l, _ = T.train_loop(X_train[i], y_train[i], type=type, model=local, lr=lr, epoch=epoch,
+                                   batch_size=batch_size, prox=prox, mu=mu,
+                                   lambda_reg_if=lambda_reg_if, lambda_reg=lambda_reg)
+            Ws.append(copy.deepcopy(w)['classifier.weight'])
+            losses.append(l)
+        out[0][t] = torch.sum(p * torch.tensor(losses))
+        g = Ws[0] * p[0]
+        for j in range(1, len(Ws)):
+            g = g + p[j] * Ws[j]
+        model.load_state_dict({'classifier.weight': g})
+        out[1][t], out[2][t] = T.test_loop(X_test=X_test, y_test=y_test, type=type, model=model,
+                                           batch_size=batch_size)
+    return out
+
+
+def _fedamw_par(X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
+                batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p):
+    """Harness: FedAMW with a fresh copy of the global model per client."""
+    model = T.MLP(D, num_classes).to(T.device)
+    n = np.array([len(y) for y in y_train])
+    p = torch.tensor(n / sum(n), dtype=torch.float32, requires_grad=True)
+    opt = torch.optim.SGD([p], lr_p, momentum=0.9)
+    ce = torch.nn.CrossEntropyLoss()
+    out = [torch.zeros(round) for _ in range(3)]
+    for t in range(round):
+        lr = T.update_learning_rate(t, lr, round)
+        Ws, losses = [], []
+        for i in range(len(y_train)):
+            local = copy.deepcopy(model)
+            w, l, _ = T.train_loop(X_train[i], y_train[i], type=type, model=local, lr=lr, epoch=epoch,
+                                   batch_size=batch_size, prox=prox, mu=mu,
+                                   lambda_reg_if=lambda_reg_if, lambda_reg=lambda_reg)
+            Ws.append(copy.deepcopy(w)['classifier.weight'])
+            losses.append(l)
+        out[0][t] = torch.sum(p * torch.tensor(losses)).detach()
+        Wst = torch.stack(Ws, dim=2)                      # [C, D, N]
+        for _ in range(round):
+            for data, label in validloader:
+                opt.zero_grad()
+                o = torch.matmul(torch.matmul(Wst.permute(2, 0, 1), data.T).permute(2, 1, 0), p)
+                ce(o, label).backward()
+                opt.step()
+        with torch.no_grad():
+            g = Ws[0] * p[0]
+            for j in range(1, len(Ws)):
+                g = g + p[j] * Ws[j]
+        model.load_state_dict({'classifier.weight': g})
+        out[1][t], out[2][t] = T.test_loop(X_test=X_test, y_test=y_test, type=type, model=model,
+                                           batch_size=batch_size)
+    return out
+
+
+CASES = [
+    # name, algo, mode, data kwargs, hyper-parameters
+    ('fedavg_seq', 'fedavg', 'seq', dict(seed=1, sizes=[45, 32, 7], n_test=50, n_raw=12, D=64, C=3),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=False, lam=0.0, R=3)),
+    ('fedprox_seq', 'fedprox', 'seq', dict(seed=2, sizes=[33, 64, 1, 20], n_test=61, n_raw=10, D=64, C=7),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=True, mu=0.05, reg=False, lam=0.0, R=4)),
+    ('fedprox_reg_seq', 'fedprox', 'seq', dict(seed=3, sizes=[40, 25, 70], n_test=47, n_raw=14, D=96, C=10),
+     dict(lr=0.3, epoch=2, batch_size=32, prox=True, mu=0.01, reg=True, lam=0.002, R=4)),
+    ('fedavg_reg_seq', 'fedavg', 'seq', dict(seed=4, sizes=[31, 9], n_test=33, n_raw=8, D=32, C=2),
+     dict(lr=0.5, epoch=3, batch_size=32, prox=False, mu=0.0, reg=True, lam=0.001, R=2)),
+    ('fedamw_seq', 'fedamw', 'seq', dict(seed=5, sizes=[50, 30, 41], n_test=40, n_raw=10, D=48, C=3, val_frac=0.2),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=3, lr_p=0.05)),
+    ('fedavg_par', 'fedavg', 'par', dict(seed=6, sizes=[45, 32, 7, 64], n_test=50, n_raw=12, D=64, C=4),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=False, lam=0.0, R=3)),
+    ('fedprox_par', 'fedprox', 'par', dict(seed=7, sizes=[33, 65, 1, 20, 96], n_test=61, n_raw=10, D=128, C=7),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=True, mu=0.05, reg=True, lam=0.001, R=4)),
+    ('fedamw_par', 'fedamw', 'par', dict(seed=8, sizes=[50, 30, 41, 66], n_test=40, n_raw=10, D=64, C=5, val_frac=0.2),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=3, lr_p=0.05)),
+]
+
+TORCH_SEED = 100   # exp.py:28
+
+
+def run_case(name, algo, mode, dk, hp):
+    d = synth(**dk)
+    Xs, ys, Xt, yt = _split(d)
+    C, D = dk['C'], dk['D']
+    _trace['W'].clear()
+    _trace['p'].clear()
+    args = (Xs, ys, Xt, yt)
+    pos = ('classification', C, D, hp['lr'], hp['epoch'], hp['batch_size'], hp['prox'], hp['mu'],
+           hp['reg'], hp['lam'], hp['R'])
+    torch.manual_seed(TORCH_SEED)
+    with contextlib.redirect_stdout(io.StringIO()):
+        if algo in ('fedavg', 'fedprox'):
+            fn = {'seq': T.FedAvg if algo == 'fedavg' else T.FedProx, 'par': _fed_par}[mode]
+            tr, tl, ta = fn(*args, *pos)
+        else:
+            vl = torch.utils.data.DataLoader(
+                torch.utils.data.TensorDataset(torch.from_numpy(d['X_val']), torch.from_numpy(d['y_val'])),
+                batch_size=16, shuffle=True)
+            fn = {'seq': T.FedAMW, 'par': _fedamw_par}[mode]
+            tr, tl, ta = fn(*args, vl, *pos, hp['lr_p'])
+    rec = dict(d)
+    rec.update({k: np.asarray(v) for k, v in hp.items()})
+    rec.update(algo=algo, mode=mode, C=C, D=D, torch_seed=TORCH_SEED,
+               train_loss=tr.detach().numpy(), test_loss=tl.numpy(), test_acc=ta.numpy(),
+               W=np.stack(_trace['W']))
+    if _trace['p']:
+        rec['p'] = np.stack(_trace['p'])
+    np.savez_compressed(os.path.join(OUT, name + '.npz'), **rec)
+    print(name, 'acc', np.round(ta.numpy(), 2), 'loss', np.round(tr.detach().numpy(), 4))
+
+
+def run_units():
+    """One train_loop call from a random start (4 prox/reg combos) and one test_loop call."""
+    d = synth(seed=11, sizes=[77], n_test=70, n_raw=12, D=96, C=6)
+    X = torch.from_numpy(d['X_train'])
+    y = torch.from_numpy(d['y_train'])
+    for prox in (False, True):
+        for reg in (False, True):
+            torch.manual_seed(123)
+            model = T.MLP(96, 6)
+            with torch.no_grad():
+                model.classifier.weight.add_(0.05 * torch.randn(6, 96))  # move off init so ||W-W_a|| path is exercised
+            W0 = model.classifier.weight.detach().clone().numpy()
+            torch.manual_seed(7)
+            w, loss, _ = T.train_loop(X, y, 'classification', model, 0.7, 3, 32, prox, 0.05, reg, 0.003)
+            np.savez_compressed(os.path.join(OUT, 'unit_train_p%d_r%d.npz' % (prox, reg)),
+                                X=d['X_train'], y=d['y_train'], W0=W0, W=w['classifier.weight'].numpy(),
+                                loss=np.float64(loss), lr=0.7, epoch=3, batch_size=32, prox=prox,
+                                mu=0.05, reg=reg, lam=0.003, seed=7)
+    torch.manual_seed(5)
+    model = T.MLP(96, 6)
+    W = model.classifier.weight.detach().clone().numpy()
+    torch.manual_seed(9)
+    with contextlib.redirect_stdout(io.StringIO()):
+        tl, ta = _orig_test_loop(torch.from_numpy(d['X_test']), torch.from_numpy(d['y_test']),
+                                 'classification', model, 32)
+    np.savez_compressed(os.path.join(OUT, 'unit_test.npz'), X=d['X_test'], y=d['y_test'], W=W,
+                        loss=np.float64(tl), acc=np.float64(ta), seed=9)
+    # init draw pattern: MLP(D, C) after manual_seed
+    torch.manual_seed(31)
+    m = T.MLP(40, 3)
+    np.savez_compressed(os.path.join(OUT, 'unit_init.npz'), W=m.classifier.weight.detach().numpy(),
+                        seed=31, D=40, C=3, after=torch.empty(3, dtype=torch.int64).random_().numpy())
+
+
+if __name__ == '__main__':
+    run_units()
+    for case in CASES:
+        run_case(*case)

@@ -1,0 +1,69 @@
+"""The CPU oracle (oracle/fedsim_oracle.py) against the reference's golden vectors."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fedsim_oracle as O
+from tests.fixtures import (LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
+                            positional, split_clients)
+
+
+def run_oracle(d):
+    Xs, ys = split_clients(d)
+    mode = 'parallel' if str(d['mode']) == 'par' else 'sequential'
+    torch.manual_seed(int(d['torch_seed']))
+    if str(d['algo']) == 'fedamw':
+        return O.FedAMW(Xs, ys, d['X_test'], d['y_test'], d['X_val'], d['y_val'], *positional(d),
+                        lr_p=float(d['lr_p']), clients=mode)
+    fn = O.FedAvg if str(d['algo']) == 'fedavg' else O.FedProx
+    return fn(Xs, ys, d['X_test'], d['y_test'], *positional(d), clients=mode)
+
+
+@pytest.mark.parametrize('name', ROUND_CASES)
+def test_round_drivers_match_reference(name):
+    d = load(name)
+    tr, tl, ta, trace = run_oracle(d)
+    W, Wref = trace['W'], d['W']
+    assert W.shape == Wref.shape
+    for t in range(W.shape[0]):
+        assert np.abs(W[t] - Wref[t]).max() <= W_RTOL * np.abs(Wref[t]).max(), (name, t)
+    np.testing.assert_allclose(tr, d['train_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl, d['test_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)
+    if 'p' in d:
+        assert np.abs(trace['p'] - d['p']).max() <= P_RTOL * np.abs(d['p']).max()
+
+
+@pytest.mark.parametrize('name', TRAIN_UNITS)
+def test_train_loop_unit(name):
+    d = load(name)
+    torch.manual_seed(int(d['seed']))
+    W, loss = O.train_client(d['X'], d['y'], d['W0'], float(d['lr']), int(d['epoch']), int(d['batch_size']),
+                             bool(d['prox']), float(d['mu']), bool(d['reg']), float(d['lam']))
+    assert np.abs(W - d['W']).max() <= 1e-6 * np.abs(d['W']).max()
+    assert abs(loss - float(d['loss'])) <= 1e-6 * max(1.0, abs(float(d['loss'])))
+
+
+def test_test_loop_unit():
+    d = load('unit_test')
+    torch.manual_seed(int(d['seed']))
+    loss, acc = O.test_eval(d['X'], d['y'], d['W'], 32)
+    assert abs(loss - float(d['loss'])) <= 1e-6
+    assert abs(acc - float(d['acc'])) <= 1e-4
+
+
+def test_init_draw_pattern():
+    d = load('unit_init')
+    torch.manual_seed(int(d['seed']))
+    W = O.mlp_init(int(d['D']), int(d['C']))
+    np.testing.assert_array_equal(W, d['W'])
+    np.testing.assert_array_equal(torch.empty(3, dtype=torch.int64).random_().numpy(), d['after'])
+
+
+def test_lr_schedule_compounds():
+    lr, seq = 0.5, []
+    for t in range(100):
+        lr = O.lr_schedule(t, lr, 100)
+        seq.append(lr)
+    assert seq[0] == 0.5 and seq[49] == 0.5
+    assert abs(seq[50] - 0.05) < 1e-15 and abs(seq[75] - 0.0005) < 1e-15 and abs(seq[99] - 0.0005) < 1e-15
