@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: client-rounds/s of the federated round on MI355X (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo fedavg|fedprox|fedamw]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+One step = one federated round with parallel clients (every client of the round
+trains from the global model): per-client local SGD (fs_local_train), weighted
+aggregation (fs_aggregate; + one RCCL all-reduce of the C x D partial aggregate
+when N > 1), test evaluation (fs_eval), and the host's RNG replay of every shuffle.
+Workload per GPU = config 2: 100 non-IID (label-skewed) a9a-shaped clients x 512
+rows, random-feature dim 2048, 10 classes, E = 2, B = 32, 10,000 test rows.
+Weak scaling: each rank owns 100 clients, so the job simulates 100 * N clients.
+Inputs are resident in HBM before the timed region; `value` = all ranks' client
+rounds / the max-over-ranks wall time of the K timed rounds.
+
+Extra objects on the JSON line:
+  roofline      fs_local_train (the dominant kernel): algorithmic HBM bytes per launch
+                (4*E*sum(n_j)*D + 8*E*sum(n_j) + 8*N*C*D) / mean launch time
+                from HIP events on the launch stream, against 8 TB/s; `traffic` = PMC HBM
+                bytes per launch from profiles/ (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE) or null.
+  cpu_baseline  the CPU oracle (oracle/fedsim_oracle.py, numpy restatement of the
+                reference round) timed on this host on whole rounds of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import fedamw_amd  # noqa: E402
+from fedamw_amd import data as fdata  # noqa: E402
+from fedamw_amd.functions import tools  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--algo', default='fedavg', choices=['fedavg', 'fedprox', 'fedamw'])
+    ap.add_argument('--clients', type=int, default=100, help='clients per GPU')
+    ap.add_argument('--rows', type=int, default=512, help='training rows per client')
+    ap.add_argument('--D', type=int, default=2048)
+    ap.add_argument('--C', type=int, default=10)
+    ap.add_argument('--test', type=int, default=10000)
+    ap.add_argument('--shape', default='a9a', choices=['a9a', 'covtype'])
+    ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the CPU baseline sample')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(d, args, budget):
+    """Whole FedAvg rounds of the same workload through the numpy oracle (rank 0 only)."""
+    from oracle import fedsim_oracle as O
+    from threadpoolctl import threadpool_info
+    Xs = [x.cpu().numpy() for x in d['X_train']]
+    ys = [y.cpu().numpy() for y in d['y_train']]
+    Xt, yt = d['X_test'].cpu().numpy(), d['y_test'].cpu().numpy()
+    p = O._weights(ys)
+    W = O.mlp_init(args.D, args.C)
+    state = torch.get_rng_state()
+    torch.manual_seed(1234)
+    rounds, clients_done = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        Ws = []
+        for X, y in zip(Xs, ys):
+            Wj, _ = O.train_client(X, y, W, 0.5, 2, 32, args.algo == 'fedprox', 5e-4, False, 0.0)
+            Ws.append(Wj)
+            clients_done += 1
+        W = O.aggregate(Ws, p)
+        O.test_eval(Xt, yt, W)
+        rounds += 1
+        el = time.perf_counter() - t0
+        if el >= budget:
+            break
+    torch.set_rng_state(state)
+    threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
+    return {'value': clients_done / el, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
+            'sample': '%d whole round(s) (%d clients x %d rows, D=%d, C=%d, E=2, B=32, aggregate + %d-row test eval) '
+                      'of the numpy oracle, %.1f s' % (rounds, len(Xs), args.rows, args.D, args.C, len(yt), el)}
+
+
+def load_traffic(kernel='local_train'):
+    path = os.path.join(ROOT, 'profiles', 'traffic_%s.json' % kernel)
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    args = parse()
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if ws > 1:
+        tdist.init_process_group('nccl', device_id=dev)
+    N_loc = args.clients
+    E, B = 2, 32
+    if args.algo == 'fedamw' and ws > 1:
+        raise SystemExit('bench: --algo fedamw pools one validation set; run it with --gpus 1')
+    # every rank synthesises the full job's clients' identities but keeps only its own rows
+    d = fdata.federated(N_loc, args.rows, args.D, args.C, args.test,
+                        n_val=(args.rows // 4 if args.algo == 'fedamw' else 0), shape=args.shape,
+                        seed=1000 + rank, device=dev)
+    # the job's client list: Federation shards clients by LPT; this rank's synthetic clients are
+    # placed at the positions it will own, the other ranks' rows are never touched here.
+    from fedamw_amd import dist as fdist
+    N_all = N_loc * ws
+    shards = fdist.shard_lpt(fdist.client_work(np.full(N_all, args.rows), E, B), ws)
+    Xs = [None] * N_all
+    ys = [torch.empty(args.rows, dtype=torch.int64)] * N_all
+    for k, j in enumerate(shards[rank]):
+        Xs[j], ys[j] = d['X_train'][k], d['y_train'][k]
+    lr, mu = 0.5, (5e-4 if args.algo == 'fedprox' else 0.0)
+    R = args.warmup + args.steps
+    vl = None
+    if args.algo == 'fedamw':
+        vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(d['X_val'], d['y_val']), batch_size=16,
+                                         shuffle=True)
+    torch.manual_seed(100)
+    fed = tools.Federation(args.algo, Xs, ys, d['X_test'], d['y_test'], vl, 'classification', args.C, args.D, lr,
+                           E, B, args.algo == 'fedprox', mu, args.algo == 'fedamw', 1e-5, R, 1e-3,
+                           'parallel', verbose=False)
+    assert len(fed.mine) == N_loc
+    ev_pairs = []
+
+    def before():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev_pairs.append([e, None])
+
+    def after():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev_pairs[-1][1] = e
+
+    for _ in range(args.warmup):
+        fed.round()
+    torch.cuda.synchronize()
+    fed.on_local_train = (before, after)
+    if ws > 1:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fed.round()
+    torch.cuda.synchronize()
+    if ws > 1:
+        tdist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        el = float(t.item())
+    lt_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
+    tr, tl, ta = fed.results()
+    n_rows = int(fed.feats.rows)
+    alg_bytes = 4.0 * E * n_rows * args.D + 8.0 * E * n_rows + 8.0 * N_loc * args.C * args.D
+    achieved = alg_bytes / (lt_ms * 1e-3) / 1e9
+    traffic = load_traffic()
+    out = {
+        'metric': 'client-rounds/sec (whole node)',
+        'value': N_loc * ws * args.steps / el,
+        'unit': 'client-rounds/s',
+        'n_gpus': ws,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': 1e3 * el / args.steps,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic (a9a-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)',
+        'config': {'workload': 'config 2: %s, %d clients/GPU x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
+                               'parallel clients' % (args.algo, N_loc, args.rows, args.D, args.C, E, B, args.test),
+                   'algo': args.algo, 'clients_total': N_loc * ws, 'rows_per_client': args.rows, 'D': args.D,
+                   'C': args.C, 'epochs': E, 'batch': B, 'test_rows': args.test, 'parallelism': 'clients%d' % ws},
+        'roofline': {'kernel': 'fs_local_train', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                     'traffic': (traffic or {}).get('bytes_per_launch'),
+                     'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes},
+        'final_test_acc': float(ta[fed.t - 1]),
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(d, args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

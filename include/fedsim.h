@@ -1,0 +1,124 @@
+/*
+ * fedsim.h -- C-ABI of the MI355X (gfx950) federated-round engine.
+ *
+ * The reference (Bojian-Wei/Non-IID-Distributed-Learning-with-Optimal-Mixture-Weights)
+ * is pure Python/PyTorch and has no native interface; every entry point below
+ * replaces one Python-level piece of its hot path, cited as
+ * /root/reference/<file>:<line>.  The Python drop-ins in
+ * non-iid-distributed-learning-with-optimal-mixture-weights_amd/functions/tools.py
+ * (FedAvg / FedProx / FedAMW) are the callers; INTEGRATION.md shows the ctypes
+ * binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Pointers named d_* are DEVICE pointers
+ *     (hipMalloc / torch caching allocator); h_* are host pointers.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All
+ *     device entry points are asynchronous on that stream, allocate nothing and
+ *     never synchronise (safe under hipGraph capture).
+ *   - Feature rows are fp32, row-major, with a leading dimension `ld` that is a
+ *     multiple of 64 floats (D is zero-padded to ld; padded columns stay exactly 0).
+ *   - Return value: 0 on success, negative on error; fs_last_error() returns a
+ *     thread-local message.  No C++ exception crosses the ABI.
+ */
+#ifndef FEDSIM_H
+#define FEDSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS_OK 0
+#define FS_EINVAL (-1)
+#define FS_EHIP (-2)
+#define FS_EUNSUPPORTED (-3)
+
+#define FS_ABI_VERSION 1
+
+/* ABI version and the last error message of the calling thread. */
+int fs_abi_version(void);
+const char* fs_last_error(void);
+
+/* ------------------------------------------------------------------------- *
+ * Host: DataLoader shuffle replay.
+ * Replaces the RandomSampler permutation of every shuffled pass
+ * (torch.utils.data.DataLoader(shuffle=True) at tools.py:179, 220; exp.py:99):
+ * for pass i, out[off[i] .. off[i]+n[i]) = torch.randperm(n[i], generator=g)
+ * with g.manual_seed(seed[i]) -- MT19937 seeded with (uint32)seed, forward
+ * Fisher-Yates with z = mt() % (n-k).  Bit-exact with torch 2.10 CPU.
+ * nthreads <= 0 picks the hardware concurrency.
+ * ------------------------------------------------------------------------- */
+int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, const int64_t* h_off,
+                      int64_t npasses, int32_t* h_out, int nthreads);
+
+/* ------------------------------------------------------------------------- *
+ * Local training of N clients.  Replaces train_loop (tools.py:177-215) called
+ * once per client by FedAvg/FedProx/FedAMW (tools.py:340-343, 367-370, 430-433).
+ *
+ *   d_phi      [rows][ld]      client features, client j = rows d_row_off[j] .. d_row_off[j+1]-1
+ *   d_row_off  [N+1]  int64    CSR row offsets
+ *   d_labels   [rows] int32    class index per row
+ *   d_perms    [E*rows] int32  client j, epoch e: local indices at E*row_off[j] + e*n_j
+ *   d_order    [N] int32       block -> client schedule (parallel mode; NULL = identity)
+ *   d_W_start  [C][ld]         round-start weights (client 0's start when chained)
+ *   d_W_out    [N][C][ld]      each client's trained weights (the clients x params buffer)
+ *   d_loss     [N] double      last-epoch |b|-weighted mean loss (incl. prox/ridge terms)
+ *   B, E       batch size (<= 64), local epochs
+ *   lr, mu, lam, prox, reg     SGD lr; prox weight (used iff prox); ridge weight (iff reg)
+ *   chained    1: client j starts from client j-1's result and its prox anchor is
+ *              that start (reference semantics);  0: every client starts
+ *              from d_W_start (parallel clients).
+ * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
+ * ------------------------------------------------------------------------- */
+int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
+                   const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
+                   float lr, float mu, int prox, float lam, int reg, int chained,
+                   const float* d_W_start, float* d_W_out, double* d_loss, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Weighted aggregation: d_W_bar = p0*W0 + p1*W1 + ... + p_{N-1}*W_{N-1}, every
+ * product and sum rounded separately in that left-to-right order
+ * (tools.py:345-350, 372-377, 455-460).  W_j = d_W_all + j*stride, len floats.
+ * chunks == 1 gives the reference's exact fold; chunks > 1 folds `chunks`
+ * consecutive client ranges in parallel and then folds the partials in order
+ * (needs d_ws of chunks*len floats).  chunks <= 0 picks a value from the shape.
+ * ------------------------------------------------------------------------- */
+int fs_aggregate(const float* d_W_all, int64_t stride, const float* d_p, int N, int64_t len,
+                 float* d_W_bar, float* d_ws, int64_t ws_floats, int chunks, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Test evaluation.  Replaces test_loop + comp_accuracy + Meter (tools.py:218-237,
+ * 82-96, 99-148): d_out[0] = mean cross-entropy over n rows, d_out[1] = top-1
+ * accuracy in percent.  Ties in the arg-max go to the lowest class index.
+ * d_ws needs fs_eval_ws_doubles(n) doubles.
+ * ------------------------------------------------------------------------- */
+int64_t fs_eval_ws_doubles(int n);
+int fs_eval(const float* d_phi, int64_t ld, const int32_t* d_labels, int n, const float* d_W, int C,
+            double* d_out, double* d_ws, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * FedAMW mixture step 1: Z[v][c*N + n] = sum_d X_val[v][d] * W_n[c][d]
+ * (the inner matmul of tools.py:448, hoisted out of the p-SGD loop because the
+ * stacked W of tools.py:435-440 is fixed during it).  fp32 MFMA GEMM.
+ * ------------------------------------------------------------------------- */
+int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val,
+             float* d_Z, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * FedAMW mixture step 2: `epochs` passes of SGD(momentum) on p over the pooled
+ * validation set (tools.py:441-453): per batch of <= Bv rows (order from d_perms,
+ * [epochs][n_val]): out[b,c] = sum_n p_n Z[v_b][c*N+n]; CE mean; grad_p;
+ * buf = first ? grad : momentum*buf + grad; p -= lr_p*buf.  d_p, d_buf [N] are
+ * updated in place; *d_first (int) is read and cleared (the momentum buffer of
+ * torch.optim.SGD starts empty, tools.py:423).  One persistent workgroup.
+ * ------------------------------------------------------------------------- */
+int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
+                 int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
+                 int* d_first, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDSIM_H */

@@ -1,0 +1,78 @@
+"""ctypes binding of libfedsim.so (C-ABI declared in include/fedsim.h).
+
+``torch`` is imported first on purpose: its wheel ships ``libamdhip64.so`` with the
+same SONAME (libamdhip64.so.7) as /opt/rocm's, so the loader reuses torch's HIP
+runtime for our kernels and both share one device context, one set of streams and
+one caching allocator.  A missing library raises -- there is no fallback path.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be loaded before libfedsim.so, see above)
+
+from . import LIB_PATH
+
+_c_f32p = C.POINTER(C.c_float)
+_SIGS = {
+    'fs_abi_version': (C.c_int, []),
+    'fs_last_error': (C.c_char_p, []),
+    'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
+    'fs_local_train': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
+                                 C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]),
+    'fs_aggregate': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                               C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
+    'fs_eval_ws_doubles': (C.c_int64, [C.c_int]),
+    'fs_eval': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                          C.c_void_p, C.c_void_p]),
+    'fs_mix_z': (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                           C.c_void_p]),
+    'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                               C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
+                               C.c_void_p]),
+}
+
+EXPORTS = tuple(_SIGS)
+ABI_VERSION = 1
+
+_lib = None
+
+
+class FedsimError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the library is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FedsimError(
+                'libfedsim.so not found at %s -- build it with `python -c "import __graft_entry__ as g; g.build()"` '
+                'or `make -C <pkg>/csrc`; there is no CPU fallback' % LIB_PATH)
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        if h.fs_abi_version() != ABI_VERSION:
+            raise FedsimError('libfedsim.so ABI %d != %d' % (h.fs_abi_version(), ABI_VERSION))
+        _lib = h
+    return _lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().fs_last_error()
+        raise FedsimError('%s failed (%d): %s' % (what, status, msg.decode() if msg else ''))
+
+
+def ptr(t):
+    """Raw data pointer of a tensor (device or host) or None."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)

@@ -1,0 +1,94 @@
+// fs_aggregate -- mixture-weighted model aggregation over the clients x params buffer.
+//
+// Replaces the inline fold of /root/reference/functions/tools.py:345-350 (also 372-377,
+// 455-460):   global = p0*W0;  global = global + p_j*W_j  for j = 1..N-1,
+// every product and every sum rounded separately (no fma contraction), so with one
+// chunk the result is bitwise the reference's fold of the same W_j.
+//
+// HBM-bound streaming reduction: each thread owns one float4 of the C*ld parameters
+// and walks the clients; consecutive threads read consecutive 16 B, so every client
+// row is one coalesced sweep.  When C*ld/4 threads cannot fill the chip the client
+// range is cut into `chunks` consecutive pieces folded in parallel (stage 1) and the
+// partials are folded in order (stage 2).
+#include "common.h"
+
+namespace fs {
+
+__device__ __forceinline__ float4 fold_step(float4 acc, float p, float4 w) {
+  return make_float4(__fadd_rn(acc.x, __fmul_rn(p, w.x)), __fadd_rn(acc.y, __fmul_rn(p, w.y)),
+                     __fadd_rn(acc.z, __fmul_rn(p, w.z)), __fadd_rn(acc.w, __fmul_rn(p, w.w)));
+}
+
+__global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict__ W, int64_t stride,
+                                                       const float* __restrict__ p, int N, int64_t len4,
+                                                       int per_chunk, float* __restrict__ out,
+                                                       int64_t out_stride) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len4) return;
+  const int k = blockIdx.y;
+  const int j0 = k * per_chunk;
+  const int j1 = min(N, j0 + per_chunk);
+  const float* base = W + 4 * i;
+  const float4 w0 = ld4(base + (int64_t)j0 * stride);
+  const float p0 = p[j0];
+  float4 acc = make_float4(__fmul_rn(p0, w0.x), __fmul_rn(p0, w0.y), __fmul_rn(p0, w0.z), __fmul_rn(p0, w0.w));
+  int j = j0 + 1;
+  for (; j + 3 < j1; j += 4) {
+    const float4 a = ld4(base + (int64_t)j * stride);
+    const float4 b = ld4(base + (int64_t)(j + 1) * stride);
+    const float4 c = ld4(base + (int64_t)(j + 2) * stride);
+    const float4 d = ld4(base + (int64_t)(j + 3) * stride);
+    acc = fold_step(acc, p[j], a);
+    acc = fold_step(acc, p[j + 1], b);
+    acc = fold_step(acc, p[j + 2], c);
+    acc = fold_step(acc, p[j + 3], d);
+  }
+  for (; j < j1; ++j) acc = fold_step(acc, p[j], ld4(base + (int64_t)j * stride));
+  st4(out + (int64_t)k * out_stride + 4 * i, acc);
+}
+
+__global__ __launch_bounds__(256) void fold_partials_kernel(const float* __restrict__ part, int K, int64_t len4,
+                                                           float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len4) return;
+  float4 acc = ld4(part + 4 * i);
+  for (int k = 1; k < K; ++k) {
+    const float4 v = ld4(part + (int64_t)k * 4 * len4 + 4 * i);
+    acc = make_float4(__fadd_rn(acc.x, v.x), __fadd_rn(acc.y, v.y), __fadd_rn(acc.z, v.z), __fadd_rn(acc.w, v.w));
+  }
+  st4(out + 4 * i, acc);
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+extern "C" int fs_aggregate(const float* d_W_all, int64_t stride, const float* d_p, int N, int64_t len,
+                            float* d_W_bar, float* d_ws, int64_t ws_floats, int chunks, void* stream) {
+  FS_REQUIRE(N >= 1, "N must be >= 1");
+  FS_REQUIRE(len >= 4 && len % 4 == 0 && stride % 4 == 0 && stride >= len, "len/stride must be multiples of 4");
+  FS_REQUIRE(d_W_all && d_p && d_W_bar, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t len4 = len / 4;
+  const int64_t bx = (len4 + 255) / 256;
+  if (chunks <= 0) {
+    // aim for >= ~2048 workgroups of 256 threads while keeping >= 8 clients per chunk
+    int64_t want = (2048 + bx - 1) / bx;
+    want = std::min<int64_t>(want, std::max<int64_t>(1, N / 8));
+    chunks = (int)std::max<int64_t>(1, want);
+  }
+  if (chunks > N) chunks = N;
+  if (chunks > 1 && (!d_ws || ws_floats < (int64_t)chunks * len)) chunks = 1;
+  const int per = (N + chunks - 1) / chunks;
+  chunks = (N + per - 1) / per;
+  if (chunks == 1) {
+    hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)bx, 1), dim3(256), 0, st, d_W_all, stride, d_p, N, len4, per,
+                       d_W_bar, (int64_t)0);
+  } else {
+    hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)bx, chunks), dim3(256), 0, st, d_W_all, stride, d_p, N, len4,
+                       per, d_ws, len);
+    hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)bx), dim3(256), 0, st, d_ws, chunks, len4, d_W_bar);
+  }
+  FS_LAUNCH_CHECK();
+  return FS_OK;
+}

@@ -1,0 +1,61 @@
+// Shared helpers for the gfx950 kernels and the C-ABI wrappers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "../../include/fedsim.h"
+
+namespace fs {
+
+// ---- error plumbing (thread-local message, negative status codes) ----------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define FS_REQUIRE(cond, msg)                                                  \
+  do {                                                                         \
+    if (!(cond)) return ::fs::fail(FS_EINVAL, std::string(__func__) + ": " + (msg)); \
+  } while (0)
+
+#define FS_LAUNCH_CHECK()                                                      \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess)                                                      \
+      return ::fs::fail(FS_EHIP, std::string(__func__) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- device helpers ----------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// v_mfma_f32_16x16x4_f32: A[i][k] lane l -> i = l&15, k = l>>4; B[k][j] -> k = l>>4,
+// j = l&15; D[i][j] -> j = l&15, i = 4*(l>>4) + reg.  Exact f32 (k-ordered fma chain).
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float comp(const float4& v, int e) {
+  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+}  // namespace fs

@@ -1,0 +1,123 @@
+// fs_eval -- test-set cross-entropy and top-1 accuracy of the global model.
+//
+// Replaces test_loop + comp_accuracy + Meter (/root/reference/functions/tools.py:218-237,
+// 82-96, 99-148).  The reference walks shuffled batches of 32 and averages per-batch
+// means weighted by batch size, which equals the plain mean over all rows up to fp32
+// rounding; the shuffle only matters for the RNG stream, which the host replays.
+//
+// Each wave owns 16 test rows: logits (16 x classes) via v_mfma_f32_16x16x4_f32 over
+// the full (padded) feature dimension, then CE and arg-max per row.  Per-block partial
+// sums go to a workspace and a one-block finalizer folds them in a fixed order, so the
+// result is bitwise reproducible run to run.  HBM-bound: one read of the test features.
+#include "common.h"
+
+namespace fs {
+
+constexpr int EV_WAVES = 4;
+constexpr int EV_ROWS = 16 * EV_WAVES;
+
+template <int CT>
+__global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __restrict__ phi, int64_t ld,
+                                                           const int32_t* __restrict__ y, int n,
+                                                           const float* __restrict__ W, int C,
+                                                           double* __restrict__ part) {
+  __shared__ float zt[EV_WAVES][16][CT * 16 + 1];
+  __shared__ double wsum[EV_WAVES][2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int NT = (int)(ld >> 6);
+  const int r0 = blockIdx.x * EV_ROWS + w * 16;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* xr = (r0 + l16 < n) ? phi + (int64_t)(r0 + l16) * ld : nullptr;
+  floatx4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int T = 0; T < NT; ++T) {
+    const int64_t dof = 64 * T + 16 * lg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 xv = xr ? ld4(xr + dof + 4 * q) : zero4;
+      float4 wv[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = ct * 16 + l16;
+        wv[ct] = c < C ? ld4(W + c * ld + dof + 4 * q) : zero4;
+      }
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(comp(xv, e4), comp(wv[ct], e4), acc[ct]);
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) zt[w][4 * lg + i][ct * 16 + l16] = acc[ct][i];
+  __syncthreads();
+  double ce = 0.0, cor = 0.0;
+  if (lane < 16 && r0 + lane < n) {
+    const int r = lane;
+    const int yy = y[r0 + r];
+    float m = -INFINITY;
+    int am = 0;
+    for (int c = 0; c < C; ++c) {
+      const float z = zt[w][r][c];
+      if (z > m) { m = z; am = c; }
+    }
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(zt[w][r][c] - m);
+    ce = (double)(-(zt[w][r][yy] - m - logf(se)));
+    cor = (am == yy) ? 1.0 : 0.0;
+  }
+  ce = wave_sum(ce);
+  cor = wave_sum(cor);
+  if (lane == 0) { wsum[w][0] = ce; wsum[w][1] = cor; }
+  __syncthreads();
+  if (tid == 0) {
+    part[2 * blockIdx.x] = ((wsum[0][0] + wsum[1][0]) + wsum[2][0]) + wsum[3][0];
+    part[2 * blockIdx.x + 1] = ((wsum[0][1] + wsum[1][1]) + wsum[2][1]) + wsum[3][1];
+  }
+}
+
+__global__ __launch_bounds__(256) void eval_finalize(const double* __restrict__ part, int nb, int n,
+                                                    double* __restrict__ out) {
+  __shared__ double s[2][256];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) { a += part[2 * i]; b += part[2 * i + 1]; }
+  s[0][threadIdx.x] = a;
+  s[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      s[0][threadIdx.x] += s[0][threadIdx.x + h];
+      s[1][threadIdx.x] += s[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = s[0][0] / (double)n;
+    out[1] = 100.0 * s[1][0] / (double)n;
+  }
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+extern "C" int64_t fs_eval_ws_doubles(int n) { return 2 * (int64_t)((n + EV_ROWS - 1) / EV_ROWS) + 2; }
+
+extern "C" int fs_eval(const float* d_phi, int64_t ld, const int32_t* d_labels, int n, const float* d_W, int C,
+                       double* d_out, double* d_ws, void* stream) {
+  FS_REQUIRE(n >= 1, "n must be >= 1");
+  FS_REQUIRE(C >= 1 && C <= 32, "num_classes must be in [1, 32]");
+  FS_REQUIRE(ld >= 64 && ld % 64 == 0, "ld must be a positive multiple of 64");
+  FS_REQUIRE(d_phi && d_labels && d_W && d_out && d_ws, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nb = (n + EV_ROWS - 1) / EV_ROWS;
+  if (C <= 16)
+    hipLaunchKernelGGL((eval_kernel<1>), dim3(nb), dim3(EV_WAVES * 64), 0, st, d_phi, ld, d_labels, n, d_W, C, d_ws);
+  else
+    hipLaunchKernelGGL((eval_kernel<2>), dim3(nb), dim3(EV_WAVES * 64), 0, st, d_phi, ld, d_labels, n, d_W, C, d_ws);
+  hipLaunchKernelGGL(eval_finalize, dim3(1), dim3(256), 0, st, d_ws, nb, n, d_out);
+  FS_LAUNCH_CHECK();
+  return FS_OK;
+}

@@ -1,0 +1,75 @@
+// Host side of the C-ABI: error plumbing and the DataLoader shuffle replay.
+//
+// fs_randperm_batch reproduces, bit for bit, the permutation that
+// torch.utils.data.RandomSampler draws for one shuffled DataLoader pass
+// (/root/reference/functions/tools.py:179, 220; /root/reference/exp.py:99):
+//   g = torch.Generator(); g.manual_seed(seed); torch.randperm(n, generator=g)
+// torch's CPU generator is MT19937 seeded with (uint32)seed and its randperm is a
+// forward Fisher-Yates taking z = mt() % (n - i) (checked
+// against torch in tests/test_rng.py).  Passes are independent, so they are spread
+// over host threads.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fedsim.h"
+
+namespace fs {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+static void randperm_one(uint64_t seed, int64_t n, int32_t* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)i;
+  std::mt19937 g((uint32_t)seed);
+  for (int64_t i = 0; i + 1 < n; ++i) {
+    const int64_t z = (int64_t)(g() % (uint32_t)(n - i));
+    std::swap(out[i], out[i + z]);
+  }
+}
+
+}  // namespace fs
+
+extern "C" int fs_abi_version(void) { return FS_ABI_VERSION; }
+
+extern "C" const char* fs_last_error(void) { return fs::g_last_error.c_str(); }
+
+extern "C" int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, const int64_t* h_off, int64_t npasses,
+                                 int32_t* h_out, int nthreads) {
+  if (npasses < 0 || (npasses > 0 && (!h_seeds || !h_n || !h_off || !h_out)))
+    return fs::fail(FS_EINVAL, "fs_randperm_batch: bad arguments");
+  for (int64_t i = 0; i < npasses; ++i)
+    if (h_n[i] < 0 || h_n[i] >= (int64_t)1 << 31) return fs::fail(FS_EINVAL, "fs_randperm_batch: n out of range");
+  if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+  int64_t total = 0;
+  for (int64_t i = 0; i < npasses; ++i) total += h_n[i];
+  if (nthreads == 1 || npasses <= 1 || total < (1 << 15)) {
+    for (int64_t i = 0; i < npasses; ++i) fs::randperm_one((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
+    return FS_OK;
+  }
+  nthreads = (int)std::min<int64_t>(nthreads, npasses);
+  std::atomic<int64_t> next{0};
+  auto worker = [&]() {
+    for (;;) {
+      const int64_t i = next.fetch_add(1);
+      if (i >= npasses) return;
+      fs::randperm_one((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
+    }
+  };
+  std::vector<std::thread> pool;
+  pool.reserve(nthreads - 1);
+  for (int t = 1; t < nthreads; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  return FS_OK;
+}

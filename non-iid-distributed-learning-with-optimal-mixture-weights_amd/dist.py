@@ -1,0 +1,67 @@
+"""Client sharding across GPUs (one process per GPU, torch.distributed over RCCL).
+
+The reference simulates clients serially in one process and has no collectives
+(SURVEY.md section 2).  Here, with ``clients='parallel'``, clients are independent
+inside a round, so they are sharded across ranks and the only exchange per round
+is ONE all-reduce (sum, fp32) of the per-rank partial aggregates
+sum_{j in rank} p_j W_j  (C x ld floats; 80 KB at C=10, D=2048) -- a latency-bound
+collective over xGMI.  FedAMW additionally all-gathers the clients' weights so every
+rank runs the identical, deterministic p-solve (no broadcast needed).
+``clients='sequential'`` (the reference's chained clients) cannot shard: every rank
+runs a full replica.
+
+Everything here is host logic (who owns which client, which RNG passes it
+replays); it is exercised on CPU with the gloo backend in tests/test_dist.py.
+"""
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+
+def world():
+    """(rank, world_size) of the default process group, (0, 1) without one."""
+    if tdist.is_available() and tdist.is_initialized():
+        return tdist.get_rank(), tdist.get_world_size()
+    return 0, 1
+
+
+def client_work(ns, E, B):
+    """Dependent SGD steps per client: E * ceil(n_j / B) (the kernel's critical path)."""
+    ns = np.asarray(ns, dtype=np.int64)
+    return E * ((ns + B - 1) // B)
+
+
+def shard_lpt(work, nranks):
+    """Longest-processing-time-first assignment of clients to ranks.
+
+    Returns a list (per rank) of client indices in ascending (global) order, so that
+    each rank's partial fold visits its clients in the reference's order."""
+    work = np.asarray(work, dtype=np.int64)
+    order = np.argsort(-work, kind='stable')
+    load = np.zeros(nranks, dtype=np.int64)
+    owner = np.empty(len(work), dtype=np.int64)
+    for j in order:
+        r = int(np.argmin(load))
+        owner[j] = r
+        load[r] += work[j]
+    return [np.nonzero(owner == r)[0] for r in range(nranks)]
+
+
+def allreduce_sum_(t, group=None):
+    """In-place sum across ranks (RCCL on GPU tensors, gloo on CPU)."""
+    if world()[1] > 1:
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=group)
+    return t
+
+
+def allgather_rows(local, counts, group=None):
+    """Concatenate every rank's ``local`` rows ([k_r, ...], k_r = counts[r]) in rank order."""
+    rank, ws = world()
+    if ws == 1:
+        return local
+    kmax = int(max(counts))
+    pad = torch.zeros((kmax,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]].copy_(local)
+    bufs = [torch.empty_like(pad) for _ in range(ws)]
+    tdist.all_gather(bufs, pad, group=group)
+    return torch.cat([b[:int(c)] for b, c in zip(bufs, counts)], 0)

@@ -1,0 +1,191 @@
+"""Device-resident round engine: HBM layout + the launches of one federated round.
+
+HBM layout (one GPU; see DESIGN.md "Data layout"):
+  phi      [rows, ld]   fp32  all local clients' features, CSR by client (row_off), D zero-padded to ld % 64 == 0
+  labels   [rows]       int32
+  row_off  [N+1]        int64
+  perms    [E*rows]     int32 this round's shuffles, client j epoch e at E*row_off[j] + e*n_j
+  W_out    [N, C, ld]   fp32  the clients x params buffer (each client's trained weights)
+  W_g      [C, ld]      fp32  global model
+  Z        [n_val, C*N] fp32  FedAMW validation logits per client (row v, column c*N+n)
+Everything stays resident across rounds; per round the host only uploads the
+shuffle indices (pinned, double-buffered, async on the compute stream).
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from . import rng
+
+
+def pad_ld(D):
+    return max(64, (int(D) + 63) // 64 * 64)
+
+
+def _to_device_f32(xs, device):
+    if len(xs) == 1:
+        return xs[0].to(device=device, dtype=torch.float32, non_blocking=True)
+    if all(x.is_cuda for x in xs):
+        return torch.cat([x.to(device=device, dtype=torch.float32) for x in xs], 0)
+    return torch.cat([x.detach().to('cpu', torch.float32) for x in xs], 0).to(device, non_blocking=True)
+
+
+class Features:
+    """Rows of features packed CSR-style in HBM (``phi[rows, ld]``) plus int32 labels."""
+
+    def __init__(self, X_list, y_list, D, device, ld=None):
+        self.device = device
+        self.D = int(D)
+        self.ld = ld or pad_ld(D)
+        self.ns = np.array([int(len(y)) for y in y_list], dtype=np.int64)
+        self.row_off = np.concatenate([[0], np.cumsum(self.ns)]).astype(np.int64)
+        rows = int(self.row_off[-1])
+        self.rows = rows
+        for X in X_list:
+            if X.dim() != 2 or X.shape[1] != self.D:
+                raise ValueError('feature matrix must be [n, D=%d], got %s' % (self.D, tuple(X.shape)))
+        self.phi = torch.zeros(max(rows, 1), self.ld, device=device, dtype=torch.float32)
+        if rows:
+            self.phi[:rows, :self.D].copy_(_to_device_f32([torch.as_tensor(x) for x in X_list], device))
+            y = torch.cat([torch.as_tensor(v).reshape(-1).to('cpu', torch.int64) for v in y_list])
+            self.labels = y.to(torch.int32).to(device)
+        else:
+            self.labels = torch.zeros(1, dtype=torch.int32, device=device)
+        self.row_off_dev = torch.from_numpy(self.row_off).to(device)
+
+
+class LocalTrainer:
+    """fs_local_train for a fixed set of clients; owns the clients x params buffer."""
+
+    def __init__(self, feats, C, B, E, nthreads=0):
+        self.f = feats
+        self.C, self.B, self.E = int(C), int(B), int(E)
+        dev = feats.device
+        N = len(feats.ns)
+        self.N = N
+        self.W_out = torch.empty(N, self.C, feats.ld, device=dev, dtype=torch.float32)
+        self.loss = torch.zeros(N, device=dev, dtype=torch.float64)
+        n_perm = max(1, self.E * feats.rows)
+        self.perm_dev = torch.empty(n_perm, dtype=torch.int32, device=dev)
+        self.perm_host = [torch.empty(n_perm, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self.events = [None, None]
+        self.k = 0
+        # pass p = j*E + e  ->  (n_j, offset)
+        ns = feats.ns
+        self.pass_n = np.repeat(ns, self.E)
+        self.pass_off = (np.repeat(self.E * feats.row_off[:-1], self.E)
+                         + np.tile(np.arange(self.E), N) * np.repeat(ns, self.E)).astype(np.int64)
+        steps = self.E * ((ns + self.B - 1) // self.B)
+        order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
+        self.order = torch.from_numpy(order).to(dev)
+        self.nthreads = nthreads
+
+    def upload_perms(self, seeds):
+        """seeds: [N*E] sampler seeds of this round's local training passes (client-major)."""
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        rng.randperms(seeds, self.pass_n, self.pass_off, self.perm_host[k], self.nthreads)
+        self.perm_dev.copy_(self.perm_host[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+
+    def run(self, W_start, lr, prox, mu, reg, lam, chained):
+        f = self.f
+        L = _lib.lib()
+        _lib.check(L.fs_local_train(_lib.ptr(f.phi), f.ld, _lib.ptr(f.row_off_dev), _lib.ptr(f.labels),
+                                    _lib.ptr(self.perm_dev), None if chained else _lib.ptr(self.order),
+                                    self.N, self.C, self.B, self.E, float(lr), float(mu), int(bool(prox)),
+                                    float(lam), int(bool(reg)), int(bool(chained)), _lib.ptr(W_start),
+                                    _lib.ptr(self.W_out), _lib.ptr(self.loss), _lib.stream_ptr()),
+                   'fs_local_train')
+        return self.W_out, self.loss
+
+
+class Aggregator:
+    """fs_aggregate over a clients x params buffer."""
+
+    def __init__(self, N, C, ld, device, chunks=0):
+        self.N, self.len = int(N), int(C) * int(ld)
+        self.chunks = chunks
+        maxc = max(1, min(64, self.N))
+        self.ws = torch.empty(maxc * self.len, dtype=torch.float32, device=device)
+
+    def run(self, W_all, p, out):
+        _lib.check(_lib.lib().fs_aggregate(_lib.ptr(W_all), self.len, _lib.ptr(p), self.N, self.len, _lib.ptr(out),
+                                           _lib.ptr(self.ws), self.ws.numel(), int(self.chunks), _lib.stream_ptr()),
+                   'fs_aggregate')
+        return out
+
+
+class Evaluator:
+    """fs_eval on a resident test set."""
+
+    def __init__(self, X_test, y_test, D, C, device, ld=None):
+        self.f = Features([torch.as_tensor(X_test)], [torch.as_tensor(y_test)], D, device, ld)
+        self.C = int(C)
+        self.n = int(self.f.rows)
+        if self.n < 1:
+            raise ValueError('empty test set')
+        self.ws = torch.empty(int(_lib.lib().fs_eval_ws_doubles(self.n)), dtype=torch.float64, device=device)
+
+    def run(self, W, out2):
+        _lib.check(_lib.lib().fs_eval(_lib.ptr(self.f.phi), self.f.ld, _lib.ptr(self.f.labels), self.n, _lib.ptr(W),
+                                      self.C, _lib.ptr(out2), _lib.ptr(self.ws), _lib.stream_ptr()), 'fs_eval')
+        return out2
+
+
+class Mixture:
+    """FedAMW's mixture-weight estimation: Z GEMM + persistent p-SGD (tools.py:435-453)."""
+
+    def __init__(self, X_val, y_val, D, C, N, Bv, p0, device, ld=None, momentum=0.9, nthreads=0):
+        self.f = Features([torch.as_tensor(X_val)], [torch.as_tensor(y_val)], D, device, ld)
+        self.C, self.N, self.Bv = int(C), int(N), int(Bv)
+        self.nv = int(self.f.rows)
+        if self.nv < 1:
+            raise ValueError('empty validation set')
+        self.momentum = float(momentum)
+        self.Z = torch.empty(self.nv, self.C * self.N, dtype=torch.float32, device=device)
+        self.p = p0.to(device=device, dtype=torch.float32).clone()
+        self.buf = torch.zeros(self.N, dtype=torch.float32, device=device)
+        self.first = torch.ones(1, dtype=torch.int32, device=device)
+        self.perm_dev = None
+        self.perm_host = [None, None]
+        self.events = [None, None]
+        self.k = 0
+        self.nthreads = nthreads
+
+    def _upload(self, seeds):
+        ep = len(seeds)
+        n = ep * self.nv
+        if self.perm_dev is None or self.perm_dev.numel() < n:
+            self.perm_dev = torch.empty(max(1, n), dtype=torch.int32, device=self.Z.device)
+            self.perm_host = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self.events = [None, None]
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        rng.randperms(seeds, np.full(ep, self.nv, np.int64), np.arange(ep, dtype=np.int64) * self.nv,
+                      self.perm_host[k], self.nthreads)
+        self.perm_dev[:n].copy_(self.perm_host[k][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+
+    def solve(self, W_all, seeds, lr_p):
+        """W_all: [N, C, ld] every client's weights; seeds: sampler seeds of the round's
+        validation passes (one per inner epoch)."""
+        L = _lib.lib()
+        _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
+                              _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')
+        epochs = len(seeds)
+        if epochs:
+            self._upload(seeds)
+        _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(self.perm_dev), self.N,
+                                  self.C, self.nv, epochs, self.Bv, float(lr_p), self.momentum,
+                                  _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first),
+                                  _lib.stream_ptr()), 'fs_mix_solve')
+        return self.p

@@ -1,0 +1,47 @@
+"""The C-ABI library loads and exports every symbol include/fedsim.h declares (CPU only;
+no compute calls), and argument validation fails cleanly through fs_last_error."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import fedamw_amd
+from fedamw_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, 'include', 'fedsim.h')).read()
+    return sorted(set(re.findall(r'\b(fs_[a-z_]+)\s*\(', src)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    h = ctypes.CDLL(fedamw_amd.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(h, name), name
+
+
+def test_abi_version():
+    assert _lib.lib().fs_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize('call,needle', [
+    (lambda L: L.fs_local_train(None, 64, None, None, None, None, 1, 40, 32, 2, 0.1, 0.0, 0, 0.0, 0, 0,
+                                None, None, None, None), 'num_classes'),
+    (lambda L: L.fs_local_train(None, 100, None, None, None, None, 1, 10, 32, 2, 0.1, 0.0, 0, 0.0, 0, 0,
+                                None, None, None, None), 'ld'),
+    (lambda L: L.fs_aggregate(None, 64, None, 0, 64, None, None, 0, 1, None), 'N'),
+    (lambda L: L.fs_eval(None, 64, None, 0, None, 10, None, None, None), 'n'),
+    (lambda L: L.fs_mix_solve(None, None, None, 5, 3, 10, 1, 65, 0.1, 0.9, None, None, None, None), 'batch'),
+])
+def test_invalid_arguments_fail_without_touching_the_gpu(call, needle):
+    L = _lib.lib()
+    rc = call(L)
+    assert rc == -1
+    assert needle in L.fs_last_error().decode()

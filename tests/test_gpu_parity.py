@@ -1,0 +1,249 @@
+"""HIP path vs the reference's golden vectors and the CPU oracle (run on the MI355X box).
+
+Tolerances (fp32): see tests/fixtures.py -- global W per round within 1e-5 of max|W|,
+losses within 1e-5, accuracy within one test sample; kernel-level checks state theirs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fedsim_oracle as O
+from tests.fixtures import (LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load, positional,
+                            split_clients)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def amd():
+    import fedamw_amd
+    from fedamw_amd import _lib, engine, rng
+    from fedamw_amd.functions import tools
+    _lib.lib()
+    return type('amd', (), dict(lib=_lib, engine=engine, rng=rng, tools=tools))
+
+
+def _dl(X, y, bs=16):
+    return torch.utils.data.DataLoader(torch.utils.data.TensorDataset(torch.from_numpy(X), torch.from_numpy(y)),
+                                       batch_size=bs, shuffle=True)
+
+
+def run_dropin(amd, d, **kw):
+    Xs, ys = split_clients(d)
+    Xs = [torch.from_numpy(x) for x in Xs]
+    ys = [torch.from_numpy(y) for y in ys]
+    mode = 'parallel' if str(d['mode']) == 'par' else 'sequential'
+    stats = {'trace': True}
+    torch.manual_seed(int(d['torch_seed']))
+    Xt, yt = torch.from_numpy(d['X_test']), torch.from_numpy(d['y_test'])
+    if str(d['algo']) == 'fedamw':
+        out = amd.tools.FedAMW(Xs, ys, Xt, yt, _dl(d['X_val'], d['y_val']), *positional(d), float(d['lr_p']),
+                               clients=mode, stats=stats, verbose=False, **kw)
+    else:
+        fn = amd.tools.FedAvg if str(d['algo']) == 'fedavg' else amd.tools.FedProx
+        out = fn(Xs, ys, Xt, yt, *positional(d), clients=mode, stats=stats, verbose=False, **kw)
+    return out, stats
+
+
+@pytest.mark.parametrize('name', ROUND_CASES)
+def test_dropin_matches_reference_golden(amd, name):
+    d = load(name)
+    (tr, tl, ta), stats = run_dropin(amd, d)
+    W, Wref = stats['W_rounds'], d['W']
+    assert W.shape == Wref.shape
+    for t in range(len(Wref)):
+        err = np.abs(W[t] - Wref[t]).max()
+        assert err <= W_RTOL * np.abs(Wref[t]).max(), (name, t, err)
+    np.testing.assert_allclose(tr.numpy(), d['train_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl.numpy(), d['test_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta.numpy() - d['test_acc']).max() <= acc_tol(d)
+    if 'p' in d:
+        p = stats['p'].cpu().numpy()
+        assert np.abs(p - d['p'][-1]).max() <= P_RTOL * np.abs(d['p']).max()
+
+
+def test_dropin_consumes_rng_like_reference(amd):
+    """After the call, the global generator must be where the reference left it."""
+    d = load('fedprox_seq')
+    run_dropin(amd, d)
+    after_amd = torch.empty(4, dtype=torch.int64).random_()
+    Xs, ys = split_clients(d)
+    torch.manual_seed(int(d['torch_seed']))
+    O.FedProx(Xs, ys, d['X_test'], d['y_test'], *positional(d))
+    after_oracle = torch.empty(4, dtype=torch.int64).random_()
+    assert torch.equal(after_amd, after_oracle)
+
+
+# ----------------------------------------------------------------------------- kernels
+
+
+def _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, ld=None, seed=0):
+    """Run fs_local_train on clients Xs/ys; returns (W_out [N,C,D], loss [N]) and the seeds used."""
+    dev = torch.device('cuda')
+    C, D = W0.shape
+    feats = amd.engine.Features([torch.from_numpy(x) for x in Xs], [torch.from_numpy(y) for y in ys], D, dev, ld)
+    tr = amd.engine.LocalTrainer(feats, C, B, E)
+    torch.manual_seed(seed)
+    seeds = amd.rng.draw_pass_seeds(len(Xs) * E)
+    tr.upload_perms(seeds)
+    Wg = torch.zeros(C, feats.ld, device=dev)
+    Wg[:, :D] = torch.from_numpy(W0)
+    W, loss = tr.run(Wg, lr, prox, mu, reg, lam, chained)
+    torch.cuda.synchronize()
+    Wn = W.cpu().numpy()
+    assert np.all(Wn[:, :, D:] == 0), 'padded columns must stay exactly zero'
+    return Wn[:, :, :D], loss.cpu().numpy()
+
+
+@pytest.mark.parametrize('name', TRAIN_UNITS)
+def test_local_train_unit_golden(amd, name):
+    d = load(name)
+    W, loss = _train_via_abi(amd, [d['X']], [d['y']], d['W0'], float(d['lr']), int(d['epoch']),
+                             int(d['batch_size']), bool(d['prox']), float(d['mu']), bool(d['reg']), float(d['lam']),
+                             chained=True, seed=int(d['seed']))
+    assert np.abs(W[0] - d['W']).max() <= 2e-6 * np.abs(d['W']).max()
+    assert abs(loss[0] - float(d['loss'])) <= 2e-6 * max(1.0, abs(float(d['loss'])))
+
+
+def _rand_clients(rs, sizes, D, C):
+    Xs = [(np.cos(rs.normal(size=(n, D))) / np.sqrt(D)).astype(np.float32) for n in sizes]
+    ys = [rs.randint(0, C, size=n).astype(np.int64) for n in sizes]
+    return Xs, ys
+
+
+@pytest.mark.parametrize('D,C,B,sizes,prox,reg', [
+    (200, 10, 32, [64, 33, 1, 7, 96], True, True),        # D not a multiple of 64, tail batches 1 and 7
+    (130, 26, 32, [40, 65], False, True),                 # C > 16 (two class tiles), 'letter'-like
+    (64, 3, 16, [50, 17], True, False),                   # B = 16 (one row tile)
+    (96, 7, 64, [130, 64, 5], True, True),                # B = 64 (four row tiles)
+    (2048, 10, 32, [512, 100], True, True),               # benchmark width
+])
+@pytest.mark.parametrize('chained', [False, True])
+def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, chained):
+    rs = np.random.RandomState(D + C + B)
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    lr, mu, lam, E = 0.4, 0.03, 0.002, 2
+    W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=11)
+    torch.manual_seed(11)   # the oracle draws the same passes (client-major, epoch-minor)
+    start = W0
+    for j, (X, y) in enumerate(zip(Xs, ys)):
+        Wr, lref = O.train_client(X, y, start, lr, E, B, prox, mu, reg, lam)
+        tol = 2e-5 * max(1.0, np.abs(Wr).max())
+        assert np.abs(W[j] - Wr).max() <= tol, (j, np.abs(W[j] - Wr).max())
+        assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref))
+        if chained:
+            start = Wr
+
+
+def test_aggregate_bitexact_and_chunked(amd):
+    rs = np.random.RandomState(0)
+    N, C, D = 37, 10, 2048
+    Ws = rs.normal(size=(N, C, D)).astype(np.float32)
+    p = rs.dirichlet(np.ones(N)).astype(np.float32)
+    ref = O.aggregate(list(Ws), p)
+    dev = torch.device('cuda')
+    Wd = torch.from_numpy(Ws).to(dev)
+    pd = torch.from_numpy(p).to(dev)
+    agg1 = amd.engine.Aggregator(N, C, D, dev, chunks=1)
+    out = torch.empty(C, D, device=dev)
+    agg1.run(Wd, pd, out)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)      # bitwise the reference's fold
+    agg8 = amd.engine.Aggregator(N, C, D, dev, chunks=8)
+    agg8.run(Wd, pd, out)
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-6 * np.abs(ref).max()
+
+
+def test_eval_unit_golden(amd):
+    d = load('unit_test')
+    dev = torch.device('cuda')
+    ev = amd.engine.Evaluator(torch.from_numpy(d['X']), torch.from_numpy(d['y']), d['X'].shape[1], d['W'].shape[0],
+                              dev)
+    W = torch.zeros(d['W'].shape[0], ev.f.ld, device=dev)
+    W[:, :d['X'].shape[1]] = torch.from_numpy(d['W'])
+    out = torch.empty(2, dtype=torch.float64, device=dev)
+    ev.run(W, out)
+    loss, acc = out.cpu().numpy()
+    assert abs(loss - float(d['loss'])) <= 1e-5 * max(1, abs(float(d['loss'])))
+    assert abs(acc - float(d['acc'])) <= 100.0 / len(d['y']) + 1e-4
+
+
+def test_mix_z_and_solve_vs_oracle(amd):
+    rs = np.random.RandomState(3)
+    N, C, D, nv = 23, 5, 192, 211
+    Ws = (rs.normal(size=(N, C, D)) * 0.3).astype(np.float32)
+    Xv = (np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=nv).astype(np.int64)
+    p0 = rs.dirichlet(np.ones(N)).astype(np.float32)
+    dev = torch.device('cuda')
+    mix = amd.engine.Mixture(torch.from_numpy(Xv), torch.from_numpy(yv), D, C, N, 16, torch.from_numpy(p0), dev)
+    Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+    Wd[:, :, :D] = torch.from_numpy(Ws)
+    for rnd in range(2):
+        torch.manual_seed(40 + rnd)
+        seeds = amd.rng.draw_pass_seeds(3)
+        mix.solve(Wd, seeds, 0.05)
+        torch.cuda.synchronize()
+        Zref = np.einsum('ncd,vd->vcn', Ws, Xv).reshape(nv, C * N)
+        assert np.abs(mix.Z.cpu().numpy() - Zref).max() <= 1e-5 * np.abs(Zref).max()
+        torch.manual_seed(40 + rnd)
+        if rnd == 0:
+            pr, br = O.mixture_solve(list(Ws), Xv, yv, p0, None, 0.05, 3)
+        else:
+            pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, 0.05, 3)
+        assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
+        assert np.abs(mix.buf.cpu().numpy() - br).max() <= 1e-4 * np.abs(br).max()
+
+
+# ----------------------------------------------------------------------------- full size
+
+
+def test_fullsize_parallel_properties(amd):
+    """Benchmark shape (config 2: 100 clients x 512 rows, D=2048, C=10): size-independent
+    properties of the parallel round."""
+    rs = np.random.RandomState(5)
+    N, n, D, C, B, E = 100, 512, 2048, 10, 32, 2
+    dev = torch.device('cuda')
+    X = torch.randn(N * n, D, device=dev).cos_().mul_(D ** -0.5)
+    y = torch.randint(0, C, (N * n,), device=dev)
+    Xs = list(X.split(n))
+    ys = [v.cpu() for v in y.split(n)]
+    feats = amd.engine.Features(Xs, ys, D, dev)
+    tr = amd.engine.LocalTrainer(feats, C, B, E)
+    torch.manual_seed(1)
+    seeds = amd.rng.draw_pass_seeds(N * E)
+    tr.upload_perms(seeds)
+    W0 = torch.zeros(C, D, device=dev)
+    W0.normal_(0, 0.05)
+    # (1) lr = 0 leaves every client at the start exactly
+    W, _ = tr.run(W0, 0.0, True, 0.01, True, 0.001, False)
+    assert torch.equal(W, W0.expand_as(W))
+    # (2) clients are independent: one client alone == the same client inside the full batch (bitwise)
+    W, loss = tr.run(W0, 0.3, True, 0.01, True, 0.001, False)
+    Wfull = W.clone()
+    j = 37
+    f1 = amd.engine.Features([Xs[j]], [ys[j]], D, dev)
+    t1 = amd.engine.LocalTrainer(f1, C, B, E)
+    t1.upload_perms(seeds.reshape(N, E)[j])
+    W1, l1 = t1.run(W0, 0.3, True, 0.01, True, 0.001, False)
+    assert torch.equal(W1[0], Wfull[j]) and float(l1[0]) == float(loss[j])
+    # (3) spot-check two clients against the oracle at full width
+    torch.cuda.synchronize()
+    for j in (0, 99):
+        g_state = torch.get_rng_state()
+        # replay this client's two passes through the oracle's RNG path
+        torch.manual_seed(1)
+        torch.empty(2 * E * j, dtype=torch.int64).random_()
+        Wr, lr_ = O.train_client(Xs[j].cpu().numpy(), ys[j].numpy(), W0.cpu().numpy(), 0.3, E, B, True, 0.01, True,
+                                 0.001)
+        torch.set_rng_state(g_state)
+        assert np.abs(Wfull[j].cpu().numpy() - Wr).max() <= 2e-5 * np.abs(Wr).max()
+        assert abs(float(loss[j]) - lr_) <= 2e-5 * max(1.0, abs(lr_))
+    # (4) aggregation with equal p over identical models returns the model (to rounding)
+    agg = amd.engine.Aggregator(N, C, D, dev)
+    out = torch.empty(C, D, device=dev)
+    p = torch.full((N,), 1.0 / N, device=dev)
+    agg.run(W0.expand(N, C, D).contiguous(), p, out)
+    assert (out - W0).abs().max().item() <= 1e-6 * W0.abs().max().item()
