@@ -53,6 +53,15 @@ int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, const int64_t*
                       int64_t npasses, int32_t* h_out, int nthreads);
 
 /* ------------------------------------------------------------------------- *
+ * Device: the same shuffle replay as fs_randperm_batch, on the GPU (one wave per
+ * pass; d_seeds/d_n/d_off are device arrays of npasses int64; max_n bounds n[i] and
+ * selects an LDS-resident (max_n <= ~38K) or in-place global-memory permutation).
+ * Bit-identical to fs_randperm_batch.  Asynchronous on `stream`.
+ * ------------------------------------------------------------------------- */
+int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t* d_off, int64_t npasses,
+                       int64_t max_n, int32_t* d_out, void* stream);
+
+/* ------------------------------------------------------------------------- *
  * Local training of N clients.  Replaces train_loop (tools.py:177-215) called
  * once per client by FedAvg/FedProx/FedAMW (tools.py:340-343, 367-370, 430-433).
  *

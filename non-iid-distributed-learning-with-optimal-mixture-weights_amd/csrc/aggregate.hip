@@ -14,9 +14,13 @@
 
 namespace fs {
 
+// No fma contraction anywhere in this file: the fold must round p*W and the sum separately
+// (plain operators under this pragma; HIP's __fmul_rn/__fadd_rn are header functions whose
+// instructions keep the default contract flag and still fuse after inlining).
+#pragma clang fp contract(off)
+
 __device__ __forceinline__ float4 fold_step(float4 acc, float p, float4 w) {
-  return make_float4(__fadd_rn(acc.x, __fmul_rn(p, w.x)), __fadd_rn(acc.y, __fmul_rn(p, w.y)),
-                     __fadd_rn(acc.z, __fmul_rn(p, w.z)), __fadd_rn(acc.w, __fmul_rn(p, w.w)));
+  return make_float4(acc.x + p * w.x, acc.y + p * w.y, acc.z + p * w.z, acc.w + p * w.w);
 }
 
 __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict__ W, int64_t stride,
@@ -31,7 +35,7 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict_
   const float* base = W + 4 * i;
   const float4 w0 = ld4(base + (int64_t)j0 * stride);
   const float p0 = p[j0];
-  float4 acc = make_float4(__fmul_rn(p0, w0.x), __fmul_rn(p0, w0.y), __fmul_rn(p0, w0.z), __fmul_rn(p0, w0.w));
+  float4 acc = make_float4(p0 * w0.x, p0 * w0.y, p0 * w0.z, p0 * w0.w);
   int j = j0 + 1;
   for (; j + 3 < j1; j += 4) {
     const float4 a = ld4(base + (int64_t)j * stride);
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(256) void fold_partials_kernel(const float* __restr
   float4 acc = ld4(part + 4 * i);
   for (int k = 1; k < K; ++k) {
     const float4 v = ld4(part + (int64_t)k * 4 * len4 + 4 * i);
-    acc = make_float4(__fadd_rn(acc.x, v.x), __fadd_rn(acc.y, v.y), __fadd_rn(acc.z, v.z), __fadd_rn(acc.w, v.w));
+    acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
   }
   st4(out + 4 * i, acc);
 }

@@ -143,9 +143,12 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_kernel(const float* __re
           const float* zr = Z + (int64_t)vid[b] * CN + n;
           for (int c = 0; c < C; ++c) gp += gs[b * C + c] * zr[(int64_t)c * N];
         }
-        const float nb = first ? gp : __fadd_rn(__fmul_rn(mom, bs[n]), gp);
-        bs[n] = nb;
-        ps[n] = __fadd_rn(ps[n], __fmul_rn(-lr, nb));
+        {
+#pragma clang fp contract(off)
+          const float nb = first ? gp : mom * bs[n] + gp;   // buf.mul_(0.9).add_(grad), two roundings
+          bs[n] = nb;
+          ps[n] = ps[n] + (-lr) * nb;                         // p.add_(buf, alpha=-lr)
+        }
       }
       first = 0;
       __syncthreads();

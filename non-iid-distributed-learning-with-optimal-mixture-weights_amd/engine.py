@@ -8,14 +8,15 @@ HBM layout (one GPU; see DESIGN.md "Data layout"):
   W_out    [N, C, ld]   fp32  the clients x params buffer (each client's trained weights)
   W_g      [C, ld]      fp32  global model
   Z        [n_val, C*N] fp32  FedAMW validation logits per client (row v, column c*N+n)
-Everything stays resident across rounds; per round the host only uploads the
-shuffle indices (pinned, double-buffered, async on the compute stream).
+Everything stays resident across rounds.  Per round the host draws the shuffle
+seeds from torch's global CPU generator (one vectorised call) and uploads them
+(pinned, double-buffered, async on the compute stream); the permutations themselves
+are replayed on the GPU by fs_randperm_device.
 """
 import numpy as np
 import torch
 
 from . import _lib
-from . import rng
 
 
 def pad_ld(D):
@@ -54,10 +55,44 @@ class Features:
         self.row_off_dev = torch.from_numpy(self.row_off).to(device)
 
 
+class Shuffler:
+    """Shuffles of a fixed set of passes (sizes ns, output offsets offs), replayed on the
+    GPU each round from host-drawn seeds (fs_randperm_device)."""
+
+    def __init__(self, ns, offs, out, device):
+        self.P = int(len(ns))
+        self.max_n = int(np.max(ns)) if self.P else 0
+        self.n_dev = torch.as_tensor(np.asarray(ns, dtype=np.int64)).to(device)
+        self.off_dev = torch.as_tensor(np.asarray(offs, dtype=np.int64)).to(device)
+        self.out = out
+        self.seed_dev = torch.empty(max(1, self.P), dtype=torch.int64, device=device)
+        self.seed_host = [torch.empty(max(1, self.P), dtype=torch.int64, pin_memory=True) for _ in range(2)]
+        self.events = [None, None]
+        self.k = 0
+
+    def run(self, seeds):
+        if self.P == 0:
+            return
+        seeds = np.asarray(seeds, dtype=np.int64)
+        assert seeds.shape == (self.P,)
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        self.seed_host[k].numpy()[:] = seeds
+        self.seed_dev.copy_(self.seed_host[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        _lib.check(_lib.lib().fs_randperm_device(_lib.ptr(self.seed_dev), _lib.ptr(self.n_dev), _lib.ptr(self.off_dev),
+                                                 self.P, self.max_n, _lib.ptr(self.out), _lib.stream_ptr()),
+                   'fs_randperm_device')
+
+
 class LocalTrainer:
     """fs_local_train for a fixed set of clients; owns the clients x params buffer."""
 
-    def __init__(self, feats, C, B, E, nthreads=0):
+    def __init__(self, feats, C, B, E):
         self.f = feats
         self.C, self.B, self.E = int(C), int(B), int(E)
         dev = feats.device
@@ -67,30 +102,20 @@ class LocalTrainer:
         self.loss = torch.zeros(N, device=dev, dtype=torch.float64)
         n_perm = max(1, self.E * feats.rows)
         self.perm_dev = torch.empty(n_perm, dtype=torch.int32, device=dev)
-        self.perm_host = [torch.empty(n_perm, dtype=torch.int32, pin_memory=True) for _ in range(2)]
-        self.events = [None, None]
-        self.k = 0
         # pass p = j*E + e  ->  (n_j, offset)
         ns = feats.ns
         self.pass_n = np.repeat(ns, self.E)
         self.pass_off = (np.repeat(self.E * feats.row_off[:-1], self.E)
                          + np.tile(np.arange(self.E), N) * np.repeat(ns, self.E)).astype(np.int64)
+        self.shuffler = Shuffler(self.pass_n, self.pass_off, self.perm_dev, dev)
         steps = self.E * ((ns + self.B - 1) // self.B)
         order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
         self.order = torch.from_numpy(order).to(dev)
-        self.nthreads = nthreads
 
     def upload_perms(self, seeds):
-        """seeds: [N*E] sampler seeds of this round's local training passes (client-major)."""
-        k = self.k
-        self.k ^= 1
-        if self.events[k] is not None:
-            self.events[k].synchronize()
-        rng.randperms(seeds, self.pass_n, self.pass_off, self.perm_host[k], self.nthreads)
-        self.perm_dev.copy_(self.perm_host[k], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[k] = ev
+        """seeds: [N*E] sampler seeds of this round's local training passes (client-major);
+        the permutations are replayed on the GPU into perm_dev."""
+        self.shuffler.run(seeds)
 
     def run(self, W_start, lr, prox, mu, reg, lam, chained):
         f = self.f
@@ -140,7 +165,7 @@ class Evaluator:
 class Mixture:
     """FedAMW's mixture-weight estimation: Z GEMM + persistent p-SGD (tools.py:435-453)."""
 
-    def __init__(self, X_val, y_val, D, C, N, Bv, p0, device, ld=None, momentum=0.9, nthreads=0):
+    def __init__(self, X_val, y_val, D, C, N, Bv, p0, device, ld=None, momentum=0.9):
         self.f = Features([torch.as_tensor(X_val)], [torch.as_tensor(y_val)], D, device, ld)
         self.C, self.N, self.Bv = int(C), int(N), int(Bv)
         self.nv = int(self.f.rows)
@@ -152,28 +177,15 @@ class Mixture:
         self.buf = torch.zeros(self.N, dtype=torch.float32, device=device)
         self.first = torch.ones(1, dtype=torch.int32, device=device)
         self.perm_dev = None
-        self.perm_host = [None, None]
-        self.events = [None, None]
-        self.k = 0
-        self.nthreads = nthreads
+        self.shuffler = None
 
     def _upload(self, seeds):
         ep = len(seeds)
-        n = ep * self.nv
-        if self.perm_dev is None or self.perm_dev.numel() < n:
-            self.perm_dev = torch.empty(max(1, n), dtype=torch.int32, device=self.Z.device)
-            self.perm_host = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for _ in range(2)]
-            self.events = [None, None]
-        k = self.k
-        self.k ^= 1
-        if self.events[k] is not None:
-            self.events[k].synchronize()
-        rng.randperms(seeds, np.full(ep, self.nv, np.int64), np.arange(ep, dtype=np.int64) * self.nv,
-                      self.perm_host[k], self.nthreads)
-        self.perm_dev[:n].copy_(self.perm_host[k][:n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.events[k] = ev
+        if self.shuffler is None or self.shuffler.P != ep:
+            self.perm_dev = torch.empty(max(1, ep * self.nv), dtype=torch.int32, device=self.Z.device)
+            self.shuffler = Shuffler(np.full(ep, self.nv, np.int64), np.arange(ep, dtype=np.int64) * self.nv,
+                                     self.perm_dev, self.Z.device)
+        self.shuffler.run(seeds)
 
     def solve(self, W_all, seeds, lr_p):
         """W_all: [N, C, ld] every client's weights; seeds: sampler seeds of the round's
@@ -182,8 +194,9 @@ class Mixture:
         _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
                               _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')
         epochs = len(seeds)
-        if epochs:
-            self._upload(seeds)
+        if epochs == 0:
+            return self.p
+        self._upload(seeds)
         _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(self.perm_dev), self.N,
                                   self.C, self.nv, epochs, self.Bv, float(lr_p), self.momentum,
                                   _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first),

@@ -247,3 +247,23 @@ def test_fullsize_parallel_properties(amd):
     p = torch.full((N,), 1.0 / N, device=dev)
     agg.run(W0.expand(N, C, D).contiguous(), p, out)
     assert (out - W0).abs().max().item() <= 1e-6 * W0.abs().max().item()
+
+
+@pytest.mark.parametrize('n', [1, 2, 511, 512, 12800, 50000])
+def test_device_randperm_matches_host_and_torch(amd, n):
+    """fs_randperm_device (LDS path, and the global-memory path at n=50000) == host replay == torch."""
+    dev = torch.device('cuda')
+    torch.manual_seed(n)
+    P = 5
+    seeds = amd.rng.draw_pass_seeds(P)
+    ns = np.full(P, n, np.int64)
+    offs = np.arange(P, dtype=np.int64) * n
+    out = torch.full((P * n,), -1, dtype=torch.int32, device=dev)
+    sh = amd.engine.Shuffler(ns, offs, out, dev)
+    sh.run(seeds)
+    host = np.empty(P * n, np.int32)
+    amd.rng.randperms(seeds, ns, offs, host)
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+    g = torch.Generator()
+    g.manual_seed(int(seeds[-1]))
+    np.testing.assert_array_equal(host[-n:], torch.randperm(n, generator=g).numpy())
