@@ -27,25 +27,38 @@ __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __rest
   const int NT = (int)(ld >> 6);
   const int r0 = blockIdx.x * EV_ROWS + w * 16;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* xr = (r0 + l16 < n) ? phi + (int64_t)(r0 + l16) * ld : nullptr;
+  const bool rok = r0 + l16 < n;
+  const float* xr = phi + (int64_t)(rok ? r0 + l16 : 0) * ld;   // unconditional loads, zeroed below
   floatx4 acc[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int T = 0; T < NT; ++T) {
-    const int64_t dof = 64 * T + 16 * lg;
+  constexpr int TB = 4;   // tiles per batch of loads: 4 x 4 x (1 + CT) 16-byte loads in flight per lane
+  for (int T0 = 0; T0 < NT; T0 += TB) {
+    float4 xv[TB][4], wv[TB][4][CT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 xv = xr ? ld4(xr + dof + 4 * q) : zero4;
-      float4 wv[CT];
+    for (int h = 0; h < TB; ++h) {
+      const int T = min(T0 + h, NT - 1);
+      const int64_t dof = 64 * T + 16 * lg;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int c = ct * 16 + l16;
-        wv[ct] = c < C ? ld4(W + c * ld + dof + 4 * q) : zero4;
+      for (int q = 0; q < 4; ++q) {
+        xv[h][q] = ld4(xr + dof + 4 * q);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) wv[h][q][ct] = ld4(W + min(ct * 16 + l16, C - 1) * ld + dof + 4 * q);
       }
+    }
 #pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4)
+    for (int h = 0; h < TB; ++h) {
+      if (T0 + h >= NT) break;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma4(comp(xv, e4), comp(wv[ct], e4), acc[ct]);
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = rok ? xv[h][q] : zero4;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const float4 wq = (ct * 16 + l16 < C) ? wv[h][q][ct] : zero4;
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) acc[ct] = mfma4(comp(x, e4), comp(wq, e4), acc[ct]);
+        }
+      }
     }
   }
 #pragma unroll

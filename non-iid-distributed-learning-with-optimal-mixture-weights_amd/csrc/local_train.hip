@@ -3,25 +3,29 @@
 // Replaces train_loop (/root/reference/functions/tools.py:177-215) as called by
 // FedAvg / FedProx / FedAMW (tools.py:340-343, 367-370, 430-433).
 //
-// One 256-thread workgroup (4 waves, one per SIMD) owns one client and runs all of
-// its E * ceil(n_j / B) dependent SGD steps without leaving the kernel.  Per step:
+// One 512-thread workgroup (8 waves, two per SIMD, up to 256 VGPRs each) owns one client and runs all of
+// its E * ceil(n_j / B) dependent SGD steps without leaving the kernel.  The feature
+// dimension is cut into 64-column tiles T, dealt round-robin to the 8 waves.  Per step:
 //   forward   z = X_b W^T        v_mfma_f32_16x16x4_f32, M = batch rows (16 per tile),
-//                                N = classes (16 per tile), K = D split over the 4 waves;
-//                                X rows gathered straight from HBM by the shuffled index.
+//                                N = classes (16 per tile), K = the wave's columns; the
+//                                batch rows are gathered straight from HBM by the shuffled
+//                                index (16 B per lane, 64 contiguous bytes per row per
+//                                instruction), all of a wave's loads issued before its MFMAs.
+//   reduce    the 8 waves' partial logits are summed through LDS, one logit per thread.
 //   softmax   g = (softmax(z) - onehot) / |b|,  CE mean           (wave 0, one row per lane)
-//   backward  grad^T = X_b^T g   v_mfma_f32_16x16x4_f32, M = D (16 per tile), N = classes,
+//   backward  grad^T = X_b^T g   v_mfma_f32_16x16x4_f32, M = 16 columns, N = classes,
 //                                K = batch rows; X_b re-read (L2-resident by now).
 //   update    W -= lr * (grad + mu (W - W_a)/||W - W_a|| + lam W/||W||)
-//             fused on the MFMA output fragments; the two norms for the next step are
-//             reduced in the same pass.
-// Lane <-> element ownership: the lane that produces grad[c][d] in the backward is
-// the lane that reads W[c][d] as the forward's B operand, so W never crosses lanes
-// and chained clients (reference semantics) need no inter-lane hand-off.
+//             fused on the MFMA output fragments; the two squared norms for the next
+//             step are reduced in the same pass.
+// Lane <-> element ownership: the lane that produces grad[c][d] in the backward is the
+// lane that reads W[c][d] as the forward's B operand, so W never crosses lanes and
+// chained clients (reference semantics) need no inter-lane hand-off.
 #include "common.h"
 
 namespace fs {
 
-constexpr int LT_WAVES = 4;
+constexpr int LT_WAVES = 8;
 constexpr int LT_THREADS = LT_WAVES * kWave;
 
 struct LTParams {
@@ -39,19 +43,44 @@ struct LTParams {
   double* loss;
 };
 
+constexpr int LT_CHUNK = 2048;   // batch rows whose (row, label) are staged in LDS at once
+
 template <int RT, int CT>
 struct LTShared {
-  int rows[2][RT * 16];
-  int ylab[2][RT * 16];
-  float zpart[LT_WAVES][RT * 16][CT * 16 + 1];
+  int erow[LT_CHUNK];                 // global feature row of each staged batch position
+  int elab[LT_CHUNK];                 // its label
+  float zpart[LT_WAVES][RT * 16][CT * 16];
   float g[RT * 16][CT * 16];
   float red[2][LT_WAVES][2];
+  float cep[2][LT_WAVES];
   float pro[LT_WAVES];
 };
+
+__device__ __forceinline__ float4 mask4(float4 v, bool keep) {
+  return keep ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
 
 template <int RT, int CT>
 __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
   __shared__ LTShared<RT, CT> sh;
+  constexpr int NC = CT * 16;           // padded classes
+  constexpr int NZ = RT * 16 * NC;      // padded logits per step
+  constexpr int UF = (RT * CT >= 4) ? 1 : 2;   // forward tiles per batch of loads (register budget)
+  constexpr int UB = (RT >= 4) ? 1 : 2;        // backward tiles per batch of loads
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -62,6 +91,7 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
   const int C = P.C;
   const int B = P.B;
   const int E = P.E;
+  const int CH = (LT_CHUNK / B) * B;
   const int nclients = P.chained ? P.N : 1;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   int it = 0;  // global step counter (parity of the double-buffered LDS slots)
@@ -107,7 +137,7 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
       acc = wave_sum(acc);
       if (lane == 0) sh.pro[w] = acc;
       __syncthreads();
-      wn2 = sh.pro[0] + sh.pro[1] + sh.pro[2] + sh.pro[3];
+      for (int i = 0; i < LT_WAVES; ++i) wn2 += sh.pro[i];
     }
 
     const float* src = start;
@@ -117,23 +147,30 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
         const int par = it & 1;
         const int b0 = s * B;
         const int bc = min(B, n - b0);
-        if (tid < bc) {
-          const int li = P.perms[(int64_t)E * row0 + (int64_t)e * n + b0 + tid];
-          sh.rows[par][tid] = (int)(row0 + li);
-          sh.ylab[par][tid] = P.labels[row0 + li];
-        }
-        __syncthreads();  // B1: batch indices visible; previous step's norm partials visible
-        if (s > 0 || e > 0) {
-          pn2 = sh.red[par ^ 1][0][0] + sh.red[par ^ 1][1][0] + sh.red[par ^ 1][2][0] + sh.red[par ^ 1][3][0];
-          wn2 = sh.red[par ^ 1][0][1] + sh.red[par ^ 1][1][1] + sh.red[par ^ 1][2][1] + sh.red[par ^ 1][3][1];
+        const int cb = b0 % CH;           // position of this batch inside the staged chunk
+        if (cb == 0) {
+          // stage the next CH shuffled rows of this epoch: (global row, label) into LDS
+          __syncthreads();                // every wave is done with the previous chunk
+          const int cn = min(CH, n - b0);
+          const int32_t* pp = P.perms + (int64_t)E * row0 + (int64_t)e * n + b0;
+          for (int i = tid; i < cn; i += LT_THREADS) {
+            const int li = pp[i];
+            sh.erow[i] = (int)(row0 + li);
+            sh.elab[i] = P.labels[row0 + li];
+          }
+          __syncthreads();
         }
 
         // ---------------- forward: z = X_b W^T ----------------
+        // invalid rows (>= bc) read a valid row and are zeroed after the load, so every
+        // load is unconditional and the compiler can keep them all in flight.
         const float* xr[RT];
+        bool xok[RT];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const int r = rt * 16 + l16;
-          xr[rt] = r < bc ? P.phi + (int64_t)sh.rows[par][r] * ld : nullptr;
+          xok[rt] = r < bc;
+          xr[rt] = P.phi + (int64_t)sh.erow[cb + (xok[rt] ? r : 0)] * ld;
         }
         floatx4 acc[RT][CT];
 #pragma unroll
@@ -141,25 +178,42 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-        for (int T = w; T < NT; T += LT_WAVES) {
-          const int64_t dof = 64 * T + 16 * lg;
+        // UF tiles per iteration: all UF x 4 x (RT + CT) 16-byte loads are issued before the MFMAs
+        for (int T0 = w; T0 < NT; T0 += UF * LT_WAVES) {
+          const bool ok1 = UF > 1 && T0 + LT_WAVES < NT;
+          const int T1 = ok1 ? T0 + LT_WAVES : T0;
+          float4 xv[UF][4][RT], wv[UF][4][CT];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float4 wv[CT], xv[RT];
+          for (int h = 0; h < UF; ++h) {
+            const int64_t dof = 64 * (h ? T1 : T0) + 16 * lg;
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-              const int c = ct * 16 + l16;
-              wv[ct] = c < C ? ld4(src + c * ld + dof + 4 * q) : zero4;
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+              for (int rt = 0; rt < RT; ++rt) xv[h][q][rt] = ld4(xr[rt] + dof + 4 * q);
+#pragma unroll
+              for (int ct = 0; ct < CT; ++ct) {
+                const int c = min(ct * 16 + l16, C - 1);
+                wv[h][q][ct] = ld4(src + c * ld + dof + 4 * q);
+              }
             }
+          }
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) xv[rt] = xr[rt] ? ld4(xr[rt] + dof + 4 * q) : zero4;
+          for (int h = 0; h < UF; ++h) {
+            if (h == 1 && !ok1) break;
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
+            for (int q = 0; q < 4; ++q) {
 #pragma unroll
-              for (int rt = 0; rt < RT; ++rt)
+              for (int rt = 0; rt < RT; ++rt) xv[h][q][rt] = mask4(xv[h][q][rt], xok[rt]);
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-                  acc[rt][ct] = mfma4(comp(xv[rt], e4), comp(wv[ct], e4), acc[rt][ct]);
+              for (int ct = 0; ct < CT; ++ct) wv[h][q][ct] = mask4(wv[h][q][ct], ct * 16 + l16 < C);
+#pragma unroll
+              for (int e4 = 0; e4 < 4; ++e4)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                  for (int ct = 0; ct < CT; ++ct)
+                    acc[rt][ct] = mfma4(comp(xv[h][q][rt], e4), comp(wv[h][q][ct], e4), acc[rt][ct]);
+            }
           }
         }
 #pragma unroll
@@ -168,97 +222,124 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
           for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int i = 0; i < 4; ++i) sh.zpart[w][rt * 16 + 4 * lg + i][ct * 16 + l16] = acc[rt][ct][i];
-        __syncthreads();  // B2: partial logits from all waves
+        __syncthreads();  // B1: partial logits of all waves; previous step's norm partials
 
-        // ---------------- softmax / CE (wave 0, row = lane) ----------------
-        if (w == 0) {
-          float ce = 0.f;
-          if (lane < RT * 16) {
-            const int r = lane;
-            if (r < bc) {
-              const int y = sh.ylab[par][r];
-              float m = -INFINITY;
-              for (int c = 0; c < C; ++c) {
-                const float z = ((sh.zpart[0][r][c] + sh.zpart[1][r][c]) + sh.zpart[2][r][c]) + sh.zpart[3][r][c];
-                sh.zpart[0][r][c] = z;
-                m = fmaxf(m, z);
-              }
-              float se = 0.f;
-              for (int c = 0; c < C; ++c) se += expf(sh.zpart[0][r][c] - m);
-              const float lse = logf(se);
-              const float invb = 1.0f / (float)bc;
-              for (int c = 0; c < C; ++c) {
-                const float lp = sh.zpart[0][r][c] - m - lse;
-                sh.g[r][c] = (c == y ? -invb : 0.f) + expf(lp) * invb;
-                if (c == y) ce = -lp;
-              }
-              for (int c = C; c < CT * 16; ++c) sh.g[r][c] = 0.f;
-            } else {
-              for (int c = 0; c < CT * 16; ++c) sh.g[r][c] = 0.f;
-            }
-          }
-          ce = wave_sum(ce);
-          if (lane == 0 && e == E - 1) {
-            float loss = ce / (float)bc;                       // CrossEntropyLoss, mean
-            if (P.prox) loss = loss + P.mu * sqrtf(pn2);       // + mu * ||W - W_a||_F  (tools.py:197, 203-205)
-            if (P.reg) loss = loss + P.lam * sqrtf(wn2);       // + lambda * ||W||_F    (tools.py:201, 203, 207)
-            lsum += (double)loss * (double)bc;                 // Meter.update(loss.item(), |b|)
+        if (s > 0 || e > 0) {
+          pn2 = 0.f;
+          wn2 = 0.f;
+#pragma unroll
+          for (int i = 0; i < LT_WAVES; ++i) {
+            pn2 += sh.red[par ^ 1][i][0];
+            wn2 += sh.red[par ^ 1][i][1];
           }
         }
-        __syncthreads();  // B3: g visible
+
+        // ------- logits (fixed-order sum of the wave partials) + softmax / CE, one logit per thread -------
+        {
+          const float invb = 1.0f / (float)bc;
+          float cep = 0.f;
+          for (int idx = tid; idx < NZ; idx += LT_THREADS) {   // NC lanes of one wave hold one row
+            const int r = idx / NC, c = idx % NC;
+            float z = 0.f;
+#pragma unroll
+            for (int i = 0; i < LT_WAVES; ++i) z += sh.zpart[i][r][c];
+            const bool valid = r < bc && c < C;
+            const float m = group_max<NC>(valid ? z : -INFINITY);
+            const float se = group_sum<NC>(valid ? expf(z - m) : 0.f);
+            float gv = 0.f;
+            if (valid) {
+              const float lp = z - m - logf(se);               // log_softmax
+              const bool isy = c == sh.elab[cb + r];
+              gv = (isy ? -invb : 0.f) + expf(lp) * invb;      // d CE_mean / d z
+              if (isy) cep -= lp;
+            }
+            sh.g[r][c] = gv;
+          }
+          cep = wave_sum(cep);
+          if (lane == 0) sh.cep[par][w] = cep;
+        }
+        __syncthreads();  // B2: g and the CE partials visible
+
+        if (tid == 0 && e == E - 1) {
+          float ce = 0.f;
+          for (int i = 0; i < LT_WAVES; ++i) ce += sh.cep[par][i];
+          float loss = ce / (float)bc;                       // CrossEntropyLoss, mean
+          if (P.prox) loss = loss + P.mu * sqrtf(pn2);       // + mu * ||W - W_a||_F  (tools.py:197, 203-205)
+          if (P.reg) loss = loss + P.lam * sqrtf(wn2);       // + lambda * ||W||_F    (tools.py:201, 203, 207)
+          lsum += (double)loss * (double)bc;                 // Meter.update(loss.item(), |b|)
+        }
 
         // ---------------- backward + fused SGD/prox/ridge update ----------------
         float gB[4 * RT][CT];
         const float* xk[4 * RT];
+        bool kok[4 * RT];
 #pragma unroll
         for (int kk = 0; kk < 4 * RT; ++kk) {
           const int r = 4 * kk + lg;
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) gB[kk][ct] = sh.g[r][ct * 16 + l16];
-          xk[kk] = r < bc ? P.phi + (int64_t)sh.rows[par][r] * ld : nullptr;
+          kok[kk] = r < bc;
+          xk[kk] = P.phi + (int64_t)sh.erow[cb + (kok[kk] ? r : 0)] * ld + 4 * l16;
         }
         const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;
         const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
         const float lr = P.lr;
         float npn = 0.f, nwn = 0.f;
-        for (int T = w; T < NT; T += LT_WAVES) {
-          floatx4 ga[CT][4];
+        for (int T0 = w; T0 < NT; T0 += UB * LT_WAVES) {
+          const bool ok1 = UB > 1 && T0 + LT_WAVES < NT;
+          const int T1 = ok1 ? T0 + LT_WAVES : T0;
+          float4 xv[UB][4 * RT];
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct)
+          for (int h = 0; h < UB; ++h)
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) ga[ct][e4] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int kk = 0; kk < 4 * RT; ++kk) xv[h][kk] = ld4(xk[kk] + 64 * (h ? T1 : T0));
 #pragma unroll
-          for (int kk = 0; kk < 4 * RT; ++kk) {
-            const float4 xv = xk[kk] ? ld4(xk[kk] + 64 * T + 4 * l16) : zero4;
+          for (int h = 0; h < UB; ++h) {
+            if (h == 1 && !ok1) break;
+            const int T = h ? T1 : T0;
+            floatx4 ga[CT][4];
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
+            for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-              for (int ct = 0; ct < CT; ++ct) ga[ct][e4] = mfma4(comp(xv, e4), gB[kk][ct], ga[ct][e4]);
-          }
-          // ga[ct][e][q] = grad[c = ct*16 + l16][d = 64T + 16 lg + 4q + e]
+              for (int e4 = 0; e4 < 4; ++e4) ga[ct][e4] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) {
-            const int c = ct * 16 + l16;
-            if (c < C) {
+            for (int kk = 0; kk < 4 * RT; ++kk) {
+              const float4 x = mask4(xv[h][kk], kok[kk]);
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int64_t off = c * ld + 64 * T + 16 * lg + 4 * q;
-                const float4 wv = ld4(src + off);
-                const float4 av = P.prox ? ld4(anchor + off) : zero4;
-                float o[4];
+              for (int e4 = 0; e4 < 4; ++e4)
 #pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                  const float wc = comp(wv, e4);
-                  const float ac = comp(av, e4);
-                  float gr = ga[ct][e4][q];
-                  if (P.prox) gr = gr + (wc - ac) * sp;
-                  if (P.reg) gr = gr + wc * sr;
-                  o[e4] = wc - lr * gr;
-                  const float dp = o[e4] - ac;
-                  npn += dp * dp;
-                  nwn += o[e4] * o[e4];
+                for (int ct = 0; ct < CT; ++ct) ga[ct][e4] = mfma4(comp(x, e4), gB[kk][ct], ga[ct][e4]);
+            }
+            // ga[ct][e][q] = grad[c = ct*16 + l16][d = 64T + 16 lg + 4q + e]
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+              const int c = ct * 16 + l16;
+              if (c < C) {
+                float4 wv[4], av[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const int64_t off = c * ld + 64 * T + 16 * lg + 4 * q;
+                  wv[q] = ld4(src + off);
+                  av[q] = P.prox ? ld4(anchor + off) : zero4;
                 }
-                st4(Wj + off, make_float4(o[0], o[1], o[2], o[3]));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const int64_t off = c * ld + 64 * T + 16 * lg + 4 * q;
+                  float o[4];
+#pragma unroll
+                  for (int e4 = 0; e4 < 4; ++e4) {
+                    const float wc = comp(wv[q], e4);
+                    const float ac = comp(av[q], e4);
+                    float gr = ga[ct][e4][q];
+                    if (P.prox) gr = gr + (wc - ac) * sp;
+                    if (P.reg) gr = gr + wc * sr;
+                    o[e4] = wc - lr * gr;
+                    const float dp = o[e4] - ac;
+                    npn += dp * dp;
+                    nwn += o[e4] * o[e4];
+                  }
+                  st4(Wj + off, make_float4(o[0], o[1], o[2], o[3]));
+                }
               }
             }
           }
@@ -278,9 +359,8 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
 }
 
 template <int RT, int CT>
-static int launch_lt(const LTParams& P, int grid, hipStream_t st) {
+static void launch_lt(const LTParams& P, int grid, hipStream_t st) {
   hipLaunchKernelGGL((local_train_kernel<RT, CT>), dim3(grid), dim3(LT_THREADS), 0, st, P);
-  return 0;
 }
 
 }  // namespace fs
