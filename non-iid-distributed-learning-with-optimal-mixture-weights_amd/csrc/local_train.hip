@@ -54,6 +54,7 @@ struct LTShared {
   float red[2][LT_WAVES][2];
   float cep[2][LT_WAVES];
   float pro[LT_WAVES];
+  float pad_[2];                      // keep sizeof a multiple of 16 B: the dynamic W image follows
 };
 
 __device__ __forceinline__ float4 mask4(float4 v, bool keep) {
@@ -74,9 +75,13 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <int RT, int CT>
+// WLDS: the client's weights live in LDS for the whole local training (row stride ld + 4
+// floats, 16 B of skew per class row), so the forward's B operand and the update never touch
+// the L1/L2 path; otherwise they stay in the (L2-resident) output buffer.
+template <int RT, int CT, bool WLDS>
 __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
   __shared__ LTShared<RT, CT> sh;
+  extern __shared__ __attribute__((aligned(16))) float sW[];   // [C][ld + 4] when WLDS
   constexpr int NC = CT * 16;           // padded classes
   constexpr int NZ = RT * 16 * NC;      // padded logits per step
   constexpr int UF = (RT * CT >= 4) ? 1 : 2;   // forward tiles per batch of loads (register budget)
@@ -93,6 +98,7 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
   const int E = P.E;
   const int CH = (LT_CHUNK / B) * B;
   const int nclients = P.chained ? P.N : 1;
+  const int64_t LDW = ld + 4;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   int it = 0;  // global step counter (parity of the double-buffered LDS slots)
 
@@ -141,6 +147,18 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
     }
 
     const float* src = start;
+    if (WLDS) {
+      // lane-owned copy: every lane later reads and writes exactly these elements
+      for (int T = w; T < NT; T += LT_WAVES)
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + l16;
+          if (c < C)
+            for (int q = 0; q < 4; ++q) {
+              const int64_t off = 64 * T + 16 * lg + 4 * q;
+              st4(sW + c * LDW + off, ld4(start + c * ld + off));
+            }
+        }
+    }
     double lsum = 0.0;
     for (int e = 0; e < E; ++e) {
       for (int s = 0; s < nb; ++s, ++it) {
@@ -193,7 +211,7 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
 #pragma unroll
               for (int ct = 0; ct < CT; ++ct) {
                 const int c = min(ct * 16 + l16, C - 1);
-                wv[h][q][ct] = ld4(src + c * ld + dof + 4 * q);
+                wv[h][q][ct] = WLDS ? ld4(sW + c * LDW + dof + 4 * q) : ld4(src + c * ld + dof + 4 * q);
               }
             }
           }
@@ -319,7 +337,7 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                   const int64_t off = c * ld + 64 * T + 16 * lg + 4 * q;
-                  wv[q] = ld4(src + off);
+                  wv[q] = WLDS ? ld4(sW + (off - c * ld) + c * LDW) : ld4(src + off);
                   av[q] = P.prox ? ld4(anchor + off) : zero4;
                 }
 #pragma unroll
@@ -338,7 +356,8 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
                     npn += dp * dp;
                     nwn += o[e4] * o[e4];
                   }
-                  st4(Wj + off, make_float4(o[0], o[1], o[2], o[3]));
+                  if (WLDS) st4(sW + (off - c * ld) + c * LDW, make_float4(o[0], o[1], o[2], o[3]));
+                  else st4(Wj + off, make_float4(o[0], o[1], o[2], o[3]));
                 }
               }
             }
@@ -353,14 +372,35 @@ __global__ __launch_bounds__(LT_THREADS) void local_train_kernel(LTParams P) {
         src = Wj;
       }
     }
+    if (WLDS) {
+      for (int T = w; T < NT; T += LT_WAVES)
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + l16;
+          if (c < C)
+            for (int q = 0; q < 4; ++q) {
+              const int64_t off = 64 * T + 16 * lg + 4 * q;
+              st4(Wj + c * ld + off, ld4(sW + c * LDW + off));
+            }
+        }
+    }
     if (tid == 0) P.loss[j] = lsum / (double)n;
     __syncthreads();
   }
 }
 
 template <int RT, int CT>
-static void launch_lt(const LTParams& P, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((local_train_kernel<RT, CT>), dim3(grid), dim3(LT_THREADS), 0, st, P);
+static int launch_lt(const LTParams& P, int grid, hipStream_t st) {
+  const size_t wbytes = sizeof(float) * (size_t)P.C * (size_t)(P.ld + 4);
+  const size_t budget = 160 * 1024 - sizeof(LTShared<RT, CT>);
+  if (wbytes <= budget) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_kernel<RT, CT, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)wbytes);
+    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL((local_train_kernel<RT, CT, true>), dim3(grid), dim3(LT_THREADS), wbytes, st, P);
+  } else {
+    hipLaunchKernelGGL((local_train_kernel<RT, CT, false>), dim3(grid), dim3(LT_THREADS), 0, st, P);
+  }
+  return FS_OK;
 }
 
 }  // namespace fs
@@ -383,12 +423,14 @@ extern "C" int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_r
   const int grid = chained ? 1 : N;
   const int RT = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   const int CT = C <= 16 ? 1 : 2;
-  if (RT == 1 && CT == 1) launch_lt<1, 1>(P, grid, st);
-  else if (RT == 2 && CT == 1) launch_lt<2, 1>(P, grid, st);
-  else if (RT == 4 && CT == 1) launch_lt<4, 1>(P, grid, st);
-  else if (RT == 1 && CT == 2) launch_lt<1, 2>(P, grid, st);
-  else if (RT == 2 && CT == 2) launch_lt<2, 2>(P, grid, st);
-  else launch_lt<4, 2>(P, grid, st);
+  int rc;
+  if (RT == 1 && CT == 1) rc = launch_lt<1, 1>(P, grid, st);
+  else if (RT == 2 && CT == 1) rc = launch_lt<2, 1>(P, grid, st);
+  else if (RT == 4 && CT == 1) rc = launch_lt<4, 1>(P, grid, st);
+  else if (RT == 1 && CT == 2) rc = launch_lt<1, 2>(P, grid, st);
+  else if (RT == 2 && CT == 2) rc = launch_lt<2, 2>(P, grid, st);
+  else rc = launch_lt<4, 2>(P, grid, st);
+  if (rc != FS_OK) return rc;
   FS_LAUNCH_CHECK();
   return FS_OK;
 }

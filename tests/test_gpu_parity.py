@@ -118,7 +118,8 @@ def _rand_clients(rs, sizes, D, C):
     (130, 26, 32, [40, 65], False, True),                 # C > 16 (two class tiles), 'letter'-like
     (64, 3, 16, [50, 17], True, False),                   # B = 16 (one row tile)
     (96, 7, 64, [130, 64, 5], True, True),                # B = 64 (four row tiles)
-    (2048, 10, 32, [512, 100], True, True),               # benchmark width
+    (2048, 10, 32, [512, 100], True, True),               # benchmark width (weights resident in LDS)
+    (4000, 10, 32, [70, 33], True, True),                 # weights too large for LDS: global-memory path
 ])
 @pytest.mark.parametrize('chained', [False, True])
 def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, chained):
