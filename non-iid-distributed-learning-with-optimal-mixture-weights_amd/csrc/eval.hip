@@ -5,8 +5,10 @@
 // means weighted by batch size, which equals the plain mean over all rows up to fp32
 // rounding; the shuffle only matters for the RNG stream, which the host replays.
 //
-// Each wave owns 16 test rows: logits (16 x classes) via v_mfma_f32_16x16x4_f32 over
-// the full (padded) feature dimension, then CE and arg-max per row.  Per-block partial
+// Each 4-wave workgroup owns 16 test rows; its waves split the 64-column feature tiles
+// (2 tiles of loads in flight per wave, ~2,500 waves for 10k rows so every CU streams),
+// computing logits (16 x classes) with v_mfma_f32_16x16x4_f32; the partials are summed
+// through LDS and wave 0 computes CE and arg-max per row.  Per-block partial
 // sums go to a workspace and a one-block finalizer folds them in a fixed order, so the
 // result is bitwise reproducible run to run.  HBM-bound: one read of the test features.
 #include "common.h"
@@ -14,7 +16,7 @@
 namespace fs {
 
 constexpr int EV_WAVES = 4;
-constexpr int EV_ROWS = 16 * EV_WAVES;
+constexpr int EV_ROWS = 16;   // rows per workgroup; its 4 waves split the feature tiles
 
 template <int CT>
 __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __restrict__ phi, int64_t ld,
@@ -22,23 +24,22 @@ __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __rest
                                                            const float* __restrict__ W, int C,
                                                            double* __restrict__ part) {
   __shared__ float zt[EV_WAVES][16][CT * 16 + 1];
-  __shared__ double wsum[EV_WAVES][2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
   const int NT = (int)(ld >> 6);
-  const int r0 = blockIdx.x * EV_ROWS + w * 16;
+  const int r0 = blockIdx.x * EV_ROWS;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool rok = r0 + l16 < n;
   const float* xr = phi + (int64_t)(rok ? r0 + l16 : 0) * ld;   // unconditional loads, zeroed below
   floatx4 acc[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
-  constexpr int TB = 4;   // tiles per batch of loads: 4 x 4 x (1 + CT) 16-byte loads in flight per lane
-  for (int T0 = 0; T0 < NT; T0 += TB) {
-    float4 xv[TB][4], wv[TB][4][CT];
+  for (int T0 = w; T0 < NT; T0 += 2 * EV_WAVES) {
+    const bool ok1 = T0 + EV_WAVES < NT;
+    const int T1 = ok1 ? T0 + EV_WAVES : T0;
+    float4 xv[2][4], wv[2][4][CT];
 #pragma unroll
-    for (int h = 0; h < TB; ++h) {
-      const int T = min(T0 + h, NT - 1);
-      const int64_t dof = 64 * T + 16 * lg;
+    for (int h = 0; h < 2; ++h) {
+      const int64_t dof = 64 * (h ? T1 : T0) + 16 * lg;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         xv[h][q] = ld4(xr + dof + 4 * q);
@@ -47,8 +48,8 @@ __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __rest
       }
     }
 #pragma unroll
-    for (int h = 0; h < TB; ++h) {
-      if (T0 + h >= NT) break;
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !ok1) break;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 x = rok ? xv[h][q] : zero4;
@@ -66,28 +67,29 @@ __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) zt[w][4 * lg + i][ct * 16 + l16] = acc[ct][i];
   __syncthreads();
-  double ce = 0.0, cor = 0.0;
-  if (lane < 16 && r0 + lane < n) {
-    const int r = lane;
-    const int yy = y[r0 + r];
-    float m = -INFINITY;
-    int am = 0;
-    for (int c = 0; c < C; ++c) {
-      const float z = zt[w][r][c];
-      if (z > m) { m = z; am = c; }
+  if (w == 0) {
+    double ce = 0.0, cor = 0.0;
+    if (lane < 16 && r0 + lane < n) {
+      const int r = lane;
+      const int yy = y[r0 + r];
+      float m = -INFINITY;
+      int am = 0;
+      for (int c = 0; c < C; ++c) {
+        const float z = ((zt[0][r][c] + zt[1][r][c]) + zt[2][r][c]) + zt[3][r][c];
+        zt[0][r][c] = z;
+        if (z > m) { m = z; am = c; }
+      }
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(zt[0][r][c] - m);
+      ce = (double)(-(zt[0][r][yy] - m - logf(se)));
+      cor = (am == yy) ? 1.0 : 0.0;
     }
-    float se = 0.f;
-    for (int c = 0; c < C; ++c) se += expf(zt[w][r][c] - m);
-    ce = (double)(-(zt[w][r][yy] - m - logf(se)));
-    cor = (am == yy) ? 1.0 : 0.0;
-  }
-  ce = wave_sum(ce);
-  cor = wave_sum(cor);
-  if (lane == 0) { wsum[w][0] = ce; wsum[w][1] = cor; }
-  __syncthreads();
-  if (tid == 0) {
-    part[2 * blockIdx.x] = ((wsum[0][0] + wsum[1][0]) + wsum[2][0]) + wsum[3][0];
-    part[2 * blockIdx.x + 1] = ((wsum[0][1] + wsum[1][1]) + wsum[2][1]) + wsum[3][1];
+    ce = wave_sum(ce);
+    cor = wave_sum(cor);
+    if (lane == 0) {
+      part[2 * blockIdx.x] = ce;
+      part[2 * blockIdx.x + 1] = cor;
+    }
   }
 }
 

@@ -57,36 +57,63 @@ class Features:
 
 class Shuffler:
     """Shuffles of a fixed set of passes (sizes ns, output offsets offs), replayed on the
-    GPU each round from host-drawn seeds (fs_randperm_device)."""
+    GPU from host-drawn seeds (fs_randperm_device), on whatever stream is current.
 
-    def __init__(self, ns, offs, out, device):
+    Two output slots let round t+1's shuffles be generated on a side stream while round t
+    trains (``prepare``), ordered by events: a slot is rewritten only after the kernel
+    that consumed it has finished (``consumed``), and read only after it is ready."""
+
+    def __init__(self, ns, offs, size, device):
         self.P = int(len(ns))
         self.max_n = int(np.max(ns)) if self.P else 0
         self.n_dev = torch.as_tensor(np.asarray(ns, dtype=np.int64)).to(device)
         self.off_dev = torch.as_tensor(np.asarray(offs, dtype=np.int64)).to(device)
-        self.out = out
-        self.seed_dev = torch.empty(max(1, self.P), dtype=torch.int64, device=device)
+        self.bufs = [torch.empty(max(1, int(size)), dtype=torch.int32, device=device) for _ in range(2)]
+        self.seed_dev = [torch.empty(max(1, self.P), dtype=torch.int64, device=device) for _ in range(2)]
         self.seed_host = [torch.empty(max(1, self.P), dtype=torch.int64, pin_memory=True) for _ in range(2)]
-        self.events = [None, None]
-        self.k = 0
+        self.host_free = [None, None]
+        self.ready = [None, None]
+        self.consumed = [None, None]
 
-    def run(self, seeds):
-        if self.P == 0:
-            return
+    def prepare(self, seeds, slot, stream=None):
+        """Enqueue the shuffles for one round into ``bufs[slot]`` on ``stream`` (default: current)."""
+        stream = stream or torch.cuda.current_stream()
         seeds = np.asarray(seeds, dtype=np.int64)
         assert seeds.shape == (self.P,)
-        k = self.k
-        self.k ^= 1
-        if self.events[k] is not None:
-            self.events[k].synchronize()
-        self.seed_host[k].numpy()[:] = seeds
-        self.seed_dev.copy_(self.seed_host[k], non_blocking=True)
+        if self.host_free[slot] is not None:
+            self.host_free[slot].synchronize()
+        self.seed_host[slot].numpy()[:] = seeds
+        if self.consumed[slot] is not None:
+            stream.wait_event(self.consumed[slot])
+        with torch.cuda.stream(stream):
+            self.seed_dev[slot].copy_(self.seed_host[slot], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.host_free[slot] = ev
+            if self.P:
+                _lib.check(_lib.lib().fs_randperm_device(_lib.ptr(self.seed_dev[slot]), _lib.ptr(self.n_dev),
+                                                         _lib.ptr(self.off_dev), self.P, self.max_n,
+                                                         _lib.ptr(self.bufs[slot]), _lib.stream_ptr(stream)),
+                           'fs_randperm_device')
+            ready = torch.cuda.Event()
+            ready.record(stream)
+        self.ready[slot] = ready
+
+    def acquire(self, slot):
+        """Make the current stream wait for ``bufs[slot]`` and return it."""
+        torch.cuda.current_stream().wait_event(self.ready[slot])
+        return self.bufs[slot]
+
+    def release(self, slot):
+        """Mark ``bufs[slot]`` consumed by the work enqueued so far on the current stream."""
         ev = torch.cuda.Event()
         ev.record()
-        self.events[k] = ev
-        _lib.check(_lib.lib().fs_randperm_device(_lib.ptr(self.seed_dev), _lib.ptr(self.n_dev), _lib.ptr(self.off_dev),
-                                                 self.P, self.max_n, _lib.ptr(self.out), _lib.stream_ptr()),
-                   'fs_randperm_device')
+        self.consumed[slot] = ev
+
+    def run(self, seeds, slot=0):
+        """Synchronous-order convenience: prepare on the current stream and return the buffer."""
+        self.prepare(seeds, slot)
+        return self.acquire(slot)
 
 
 class LocalTrainer:
@@ -100,32 +127,32 @@ class LocalTrainer:
         self.N = N
         self.W_out = torch.empty(N, self.C, feats.ld, device=dev, dtype=torch.float32)
         self.loss = torch.zeros(N, device=dev, dtype=torch.float64)
-        n_perm = max(1, self.E * feats.rows)
-        self.perm_dev = torch.empty(n_perm, dtype=torch.int32, device=dev)
         # pass p = j*E + e  ->  (n_j, offset)
         ns = feats.ns
         self.pass_n = np.repeat(ns, self.E)
         self.pass_off = (np.repeat(self.E * feats.row_off[:-1], self.E)
                          + np.tile(np.arange(self.E), N) * np.repeat(ns, self.E)).astype(np.int64)
-        self.shuffler = Shuffler(self.pass_n, self.pass_off, self.perm_dev, dev)
+        self.shuffler = Shuffler(self.pass_n, self.pass_off, self.E * feats.rows, dev)
         steps = self.E * ((ns + self.B - 1) // self.B)
         order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
         self.order = torch.from_numpy(order).to(dev)
 
-    def upload_perms(self, seeds):
-        """seeds: [N*E] sampler seeds of this round's local training passes (client-major);
-        the permutations are replayed on the GPU into perm_dev."""
-        self.shuffler.run(seeds)
+    def upload_perms(self, seeds, slot=0, stream=None):
+        """seeds: [N*E] sampler seeds of one round's local training passes (client-major);
+        the permutations are replayed on the GPU into shuffle slot ``slot``."""
+        self.shuffler.prepare(seeds, slot, stream)
 
-    def run(self, W_start, lr, prox, mu, reg, lam, chained):
+    def run(self, W_start, lr, prox, mu, reg, lam, chained, slot=0):
         f = self.f
         L = _lib.lib()
+        perms = self.shuffler.acquire(slot)
         _lib.check(L.fs_local_train(_lib.ptr(f.phi), f.ld, _lib.ptr(f.row_off_dev), _lib.ptr(f.labels),
-                                    _lib.ptr(self.perm_dev), None if chained else _lib.ptr(self.order),
+                                    _lib.ptr(perms), None if chained else _lib.ptr(self.order),
                                     self.N, self.C, self.B, self.E, float(lr), float(mu), int(bool(prox)),
                                     float(lam), int(bool(reg)), int(bool(chained)), _lib.ptr(W_start),
                                     _lib.ptr(self.W_out), _lib.ptr(self.loss), _lib.stream_ptr()),
                    'fs_local_train')
+        self.shuffler.release(slot)
         return self.W_out, self.loss
 
 
@@ -176,29 +203,33 @@ class Mixture:
         self.p = p0.to(device=device, dtype=torch.float32).clone()
         self.buf = torch.zeros(self.N, dtype=torch.float32, device=device)
         self.first = torch.ones(1, dtype=torch.int32, device=device)
-        self.perm_dev = None
         self.shuffler = None
 
-    def _upload(self, seeds):
+    def prepare(self, seeds, slot=0, stream=None):
+        """Enqueue one round's validation-pass shuffles (one seed per inner epoch)."""
         ep = len(seeds)
         if self.shuffler is None or self.shuffler.P != ep:
-            self.perm_dev = torch.empty(max(1, ep * self.nv), dtype=torch.int32, device=self.Z.device)
             self.shuffler = Shuffler(np.full(ep, self.nv, np.int64), np.arange(ep, dtype=np.int64) * self.nv,
-                                     self.perm_dev, self.Z.device)
-        self.shuffler.run(seeds)
+                                     ep * self.nv, self.Z.device)
+        self.shuffler.prepare(seeds, slot, stream)
 
-    def solve(self, W_all, seeds, lr_p):
+    def solve(self, W_all, seeds, lr_p, slot=None):
         """W_all: [N, C, ld] every client's weights; seeds: sampler seeds of the round's
-        validation passes (one per inner epoch)."""
+        validation passes (one per inner epoch), or None when ``prepare`` already enqueued
+        them into ``slot``."""
         L = _lib.lib()
         _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
                               _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')
-        epochs = len(seeds)
-        if epochs == 0:
-            return self.p
-        self._upload(seeds)
-        _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(self.perm_dev), self.N,
+        if seeds is not None:
+            slot = 0
+            if len(seeds) == 0:
+                return self.p
+            self.prepare(seeds, slot)
+        epochs = self.shuffler.P
+        perms = self.shuffler.acquire(slot)
+        _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(perms), self.N,
                                   self.C, self.nv, epochs, self.Bv, float(lr_p), self.momentum,
                                   _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first),
                                   _lib.stream_ptr()), 'fs_mix_solve')
+        self.shuffler.release(slot)
         return self.p

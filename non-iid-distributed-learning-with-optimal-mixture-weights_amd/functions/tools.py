@@ -136,19 +136,34 @@ class Federation:
         self.eval_hist = torch.empty(R, 2, dtype=torch.float64, device=dev)
         self.W_hist = torch.empty(R, C, ld, device=dev) if (stats is not None and stats.get('trace')) else None
         self.n_val_pass = R if algo == 'fedamw' else 0
+        self.side = torch.cuda.Stream(device=dev)    # shuffles of round t+1 are replayed here during round t
         self.t = 0
         self.on_local_train = None      # optional (before, after) hooks around the local-training launch
 
-    def round(self):
-        """Run round t (tools.py:337-352 / 364-379 / 427-462) -- all launches async."""
-        t = self.t
+    def _prepare(self, t):
+        """Draw round t's shuffle seeds (torch's global CPU generator, in the reference's
+        order: train passes client-major, then validation passes, then the test pass) and
+        enqueue their GPU replay on the side stream into slot t % 2."""
         N, E = self.N, self.E
+        seeds = rng.draw_pass_seeds(N * E + self.n_val_pass + 1)
+        self.trainer.upload_perms(seeds[:N * E].reshape(N, E)[self.mine].reshape(-1), t % 2, self.side)
+        if self.mixture is not None:
+            self.mixture.prepare(seeds[N * E:N * E + self.n_val_pass], t % 2, self.side)
+
+    def round(self):
+        """Run round t (tools.py:337-352 / 364-379 / 427-462) -- all launches async.  The draw
+        pattern is data-independent, so drawing round t+1's seeds during round t leaves the
+        generator exactly where the reference leaves it after each call."""
+        t = self.t
+        if t == 0:
+            self._prepare(0)
+        if t + 1 < self.R:
+            self._prepare(t + 1)
         self.lr = update_learning_rate(t, self.lr, self.R)
-        seeds = rng.draw_pass_seeds(N * E + self.n_val_pass + 1)     # train passes, valid passes, test pass
-        self.trainer.upload_perms(seeds[:N * E].reshape(N, E)[self.mine].reshape(-1))
         if self.on_local_train:
             self.on_local_train[0]()
-        W_out, loss = self.trainer.run(self.W_g, self.lr, self.prox, self.mu, self.reg, self.lam, self.chained)
+        W_out, loss = self.trainer.run(self.W_g, self.lr, self.prox, self.mu, self.reg, self.lam, self.chained,
+                                       slot=t % 2)
         if self.on_local_train:
             self.on_local_train[1]()
         self.loss_hist[t].copy_(loss)
@@ -157,7 +172,7 @@ class Federation:
             W_all = W_out
             if self.sharded:
                 W_all = dist.allgather_rows(W_out, [len(s) for s in self.shards])[self.inv]
-            p = self.mixture.solve(W_all, seeds[N * E:N * E + self.n_val_pass], self.lr_p)
+            p = self.mixture.solve(W_all, None, self.lr_p, slot=t % 2)
             self.agg.run(W_all, p, self.W_g)
         else:
             self.agg.run(W_out, self.p_mine, self.W_g)

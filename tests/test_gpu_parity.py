@@ -259,9 +259,8 @@ def test_device_randperm_matches_host_and_torch(amd, n):
     seeds = amd.rng.draw_pass_seeds(P)
     ns = np.full(P, n, np.int64)
     offs = np.arange(P, dtype=np.int64) * n
-    out = torch.full((P * n,), -1, dtype=torch.int32, device=dev)
-    sh = amd.engine.Shuffler(ns, offs, out, dev)
-    sh.run(seeds)
+    sh = amd.engine.Shuffler(ns, offs, P * n, dev)
+    out = sh.run(seeds)
     host = np.empty(P * n, np.int32)
     amd.rng.randperms(seeds, ns, offs, host)
     np.testing.assert_array_equal(out.cpu().numpy(), host)
