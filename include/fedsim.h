@@ -34,7 +34,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 1
+#define FS_ABI_VERSION 2
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -78,12 +78,21 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *   chained    1: client j starts from client j-1's result and its prox anchor is
  *              that start (reference semantics);  0: every client starts
  *              from d_W_start (parallel clients).
+ *   G, d_ws    workgroups per client and their workspace, from fs_local_train_plan:
+ *              G = 1: one workgroup walks each client (any shape, chained or not);
+ *              G = 2/4: "split clients" -- G co-resident workgroups share one client's
+ *              feature tiles and exchange partial logits every step (parallel mode,
+ *              C <= 16, B <= 32, N*G <= CUs).  d_ws[0..3] is an error word: nonzero
+ *              after the kernel means the plan was violated (results invalid).
  * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
  * ------------------------------------------------------------------------- */
+int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int* G_out,
+                        int64_t* ws_bytes_out);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                    const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
                    float lr, float mu, int prox, float lam, int reg, int chained,
-                   const float* d_W_start, float* d_W_out, double* d_loss, void* stream);
+                   const float* d_W_start, float* d_W_out, double* d_loss, int G, void* d_ws,
+                   int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * Weighted aggregation: d_W_bar = p0*W0 + p1*W1 + ... + p_{N-1}*W_{N-1}, every

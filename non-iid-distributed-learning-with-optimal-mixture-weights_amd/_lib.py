@@ -19,10 +19,12 @@ _SIGS = {
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     'fs_randperm_device': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                      C.c_void_p]),
+    'fs_local_train_plan': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int,
+                                      C.c_void_p, C.c_void_p]),
     'fs_local_train': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
                                  C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                 C.c_void_p]),
+                                 C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_aggregate': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
                                C.c_void_p, C.c_int64, C.c_int, C.c_void_p]),
     'fs_eval_ws_doubles': (C.c_int64, [C.c_int]),
@@ -36,7 +38,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 
@@ -46,14 +48,16 @@ class FedsimError(RuntimeError):
 
 
 def lib():
-    """Load (once) and return the ctypes handle; raises if the library is missing."""
+    """Load (once) and return the ctypes handle; raises if the library is missing.
+    FEDSIM_LIB overrides the path (diagnostic builds, e.g. the in-kernel stamp build)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get('FEDSIM_LIB', LIB_PATH)
+        if not os.path.exists(path):
             raise FedsimError(
                 'libfedsim.so not found at %s -- build it with `python -c "import __graft_entry__ as g; g.build()"` '
-                'or `make -C <pkg>/csrc`; there is no CPU fallback' % LIB_PATH)
-        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+                'or `make -C <pkg>/csrc`; there is no CPU fallback' % path)
+        h = C.CDLL(path, mode=C.RTLD_GLOBAL)
         for name, (res, args) in _SIGS.items():
             f = getattr(h, name)
             f.restype = res

@@ -27,6 +27,25 @@ int fail(int code, const std::string& msg);
       return ::fs::fail(FS_EHIP, std::string(__func__) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// ---- local training parameters (shared by the single- and split-workgroup kernels) ----
+struct LTParams {
+  const float* phi;
+  int64_t ld;
+  const int64_t* row_off;
+  const int32_t* labels;
+  const int32_t* perms;
+  const int32_t* order;
+  int N, C, B, E;
+  float lr, mu, lam;
+  int prox, reg, chained;
+  const float* W_start;
+  float* W_out;
+  double* loss;
+};
+
+// split-client launcher (local_train_split.hip): G workgroups per client
+int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
+
 // ---- device helpers ----------------------------------------------------------
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 

@@ -28,21 +28,6 @@ namespace fs {
 constexpr int LT_WAVES = 8;
 constexpr int LT_THREADS = LT_WAVES * kWave;
 
-struct LTParams {
-  const float* phi;
-  int64_t ld;
-  const int64_t* row_off;
-  const int32_t* labels;
-  const int32_t* perms;
-  const int32_t* order;
-  int N, C, B, E;
-  float lr, mu, lam;
-  int prox, reg, chained;
-  const float* W_start;
-  float* W_out;
-  double* loss;
-};
-
 constexpr int LT_CHUNK = 2048;   // batch rows whose (row, label) are staged in LDS at once
 
 template <int RT, int CT>
@@ -410,7 +395,8 @@ using namespace fs;
 extern "C" int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                               const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
                               float lr, float mu, int prox, float lam, int reg, int chained,
-                              const float* d_W_start, float* d_W_out, double* d_loss, void* stream) {
+                              const float* d_W_start, float* d_W_out, double* d_loss, int G, void* d_ws,
+                              int64_t ws_bytes, void* stream) {
   FS_REQUIRE(N >= 1, "N must be >= 1");
   FS_REQUIRE(C >= 1 && C <= 32, "num_classes must be in [1, 32]");
   FS_REQUIRE(B >= 1 && B <= 64, "batch_size must be in [1, 64]");
@@ -420,6 +406,10 @@ extern "C" int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_r
   LTParams P{d_phi, ld, d_row_off, d_labels, d_perms, d_order, N, C, B, E, lr, mu, lam,
              prox ? 1 : 0, reg ? 1 : 0, chained ? 1 : 0, d_W_start, d_W_out, d_loss};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (G > 1) {
+    FS_REQUIRE(!chained, "split clients (G > 1) need parallel clients");
+    return launch_local_train_split(P, G, d_ws, ws_bytes, st);
+  }
   const int grid = chained ? 1 : N;
   const int RT = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   const int CT = C <= 16 ? 1 : 2;

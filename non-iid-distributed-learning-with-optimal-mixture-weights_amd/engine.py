@@ -117,9 +117,13 @@ class Shuffler:
 
 
 class LocalTrainer:
-    """fs_local_train for a fixed set of clients; owns the clients x params buffer."""
+    """fs_local_train for a fixed set of clients; owns the clients x params buffer.
 
-    def __init__(self, feats, C, B, E):
+    ``split``: workgroups per client.  None asks fs_local_train_plan (split clients when the
+    round has fewer clients than CUs and the shape allows it, parallel mode only); 1 forces
+    one workgroup per client."""
+
+    def __init__(self, feats, C, B, E, split=None, chained=False):
         self.f = feats
         self.C, self.B, self.E = int(C), int(B), int(E)
         dev = feats.device
@@ -136,6 +140,24 @@ class LocalTrainer:
         steps = self.E * ((ns + self.B - 1) // self.B)
         order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
         self.order = torch.from_numpy(order).to(dev)
+        import ctypes
+        g, wsb = ctypes.c_int(1), ctypes.c_int64(0)
+        if split != 1 and not chained:
+            max_en = int(self.E * ns.max()) if N else 0
+            _lib.check(_lib.lib().fs_local_train_plan(N, self.C, self.B, self.E, feats.ld, max_en, 0,
+                                                      ctypes.byref(g), ctypes.byref(wsb)), 'fs_local_train_plan')
+            if split is not None:          # explicit G: the launch validates it
+                g.value = int(split)
+                wsb.value = max(int(wsb.value), 1 << 20)
+        self.G = int(g.value)
+        self.ws = torch.zeros(max(256, int(wsb.value)), dtype=torch.uint8, device=dev) if self.G > 1 else None
+
+    def check_errors(self):
+        """Raise if a split-client launch reported a broken hand-off (synchronises)."""
+        if self.G > 1:
+            err = int(self.ws[:4].view(torch.int32).item())
+            if err:
+                raise _lib.FedsimError('fs_local_train: split-client hand-off failed (code %d)' % err)
 
     def upload_perms(self, seeds, slot=0, stream=None):
         """seeds: [N*E] sampler seeds of one round's local training passes (client-major);
@@ -150,7 +172,8 @@ class LocalTrainer:
                                     _lib.ptr(perms), None if chained else _lib.ptr(self.order),
                                     self.N, self.C, self.B, self.E, float(lr), float(mu), int(bool(prox)),
                                     float(lam), int(bool(reg)), int(bool(chained)), _lib.ptr(W_start),
-                                    _lib.ptr(self.W_out), _lib.ptr(self.loss), _lib.stream_ptr()),
+                                    _lib.ptr(self.W_out), _lib.ptr(self.loss), self.G, _lib.ptr(self.ws),
+                                    0 if self.ws is None else self.ws.numel(), _lib.stream_ptr()),
                    'fs_local_train')
         self.shuffler.release(slot)
         return self.W_out, self.loss

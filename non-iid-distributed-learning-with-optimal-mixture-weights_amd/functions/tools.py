@@ -113,7 +113,7 @@ class Federation:
         self.feats = engine.Features([torch.as_tensor(X_train[j]) for j in mine],
                                      [torch.as_tensor(y_train[j]) for j in mine], D, dev)
         ld = self.ld = self.feats.ld
-        self.trainer = engine.LocalTrainer(self.feats, C, B, E)
+        self.trainer = engine.LocalTrainer(self.feats, C, B, E, chained=self.chained)
         self.evaluator = engine.Evaluator(X_test, y_test, D, C, dev, ld)
         self.W_g = torch.zeros(C, ld, device=dev, dtype=torch.float32)
         self.W_g[:, :D].copy_(W_init)
@@ -186,6 +186,7 @@ class Federation:
     def results(self):
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""
         R, D = self.t, self.D
+        self.trainer.check_errors()
         loss_hist = self.loss_hist[:R]
         if self.sharded:
             loss_hist = dist.allgather_rows(loss_hist.t().contiguous(), [len(s) for s in self.shards]).t()

@@ -1,0 +1,13 @@
+# PMC passes over fs_local_train (one counter group per rocprofv3 run, each under a hard timeout).
+set -o pipefail
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS" "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-include-regex "local_train|eval_kernel" -d $OUT/p$i -o p$i --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
+  echo "pass $i ($grp) rc=$?"
+done

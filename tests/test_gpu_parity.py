@@ -79,12 +79,12 @@ def test_dropin_consumes_rng_like_reference(amd):
 # ----------------------------------------------------------------------------- kernels
 
 
-def _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, ld=None, seed=0):
-    """Run fs_local_train on clients Xs/ys; returns (W_out [N,C,D], loss [N]) and the seeds used."""
+def _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, ld=None, seed=0, split=None):
+    """Run fs_local_train on clients Xs/ys; returns (W_out [N,C,D], loss [N])."""
     dev = torch.device('cuda')
     C, D = W0.shape
     feats = amd.engine.Features([torch.from_numpy(x) for x in Xs], [torch.from_numpy(y) for y in ys], D, dev, ld)
-    tr = amd.engine.LocalTrainer(feats, C, B, E)
+    tr = amd.engine.LocalTrainer(feats, C, B, E, split=split, chained=chained)
     torch.manual_seed(seed)
     seeds = amd.rng.draw_pass_seeds(len(Xs) * E)
     tr.upload_perms(seeds)
@@ -92,6 +92,8 @@ def _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, ld=No
     Wg[:, :D] = torch.from_numpy(W0)
     W, loss = tr.run(Wg, lr, prox, mu, reg, lam, chained)
     torch.cuda.synchronize()
+    tr.check_errors()
+    _train_via_abi.last_G = tr.G
     Wn = W.cpu().numpy()
     assert np.all(Wn[:, :, D:] == 0), 'padded columns must stay exactly zero'
     return Wn[:, :, :D], loss.cpu().numpy()
@@ -121,13 +123,18 @@ def _rand_clients(rs, sizes, D, C):
     (2048, 10, 32, [512, 100], True, True),               # benchmark width (weights resident in LDS)
     (4000, 10, 32, [70, 33], True, True),                 # weights too large for LDS: global-memory path
 ])
-@pytest.mark.parametrize('chained', [False, True])
-def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, chained):
+@pytest.mark.parametrize('mode', ['chained', 'parallel-1wg', 'parallel-auto'])
+def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, mode):
+    """chained = reference semantics (one workgroup walks the chain); parallel-1wg = one
+    workgroup per client; parallel-auto = the planner's choice (split clients: G=2/4
+    workgroups per client exchanging partial logits, whenever the shape allows)."""
     rs = np.random.RandomState(D + C + B)
     Xs, ys = _rand_clients(rs, sizes, D, C)
     W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
     lr, mu, lam, E = 0.4, 0.03, 0.002, 2
-    W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=11)
+    chained = mode == 'chained'
+    W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=11,
+                             split=1 if mode == 'parallel-1wg' else None)
     torch.manual_seed(11)   # the oracle draws the same passes (client-major, epoch-minor)
     start = W0
     for j, (X, y) in enumerate(zip(Xs, ys)):
@@ -213,6 +220,7 @@ def test_fullsize_parallel_properties(amd):
     ys = [v.cpu() for v in y.split(n)]
     feats = amd.engine.Features(Xs, ys, D, dev)
     tr = amd.engine.LocalTrainer(feats, C, B, E)
+    G = tr.G
     torch.manual_seed(1)
     seeds = amd.rng.draw_pass_seeds(N * E)
     tr.upload_perms(seeds)
@@ -226,7 +234,7 @@ def test_fullsize_parallel_properties(amd):
     Wfull = W.clone()
     j = 37
     f1 = amd.engine.Features([Xs[j]], [ys[j]], D, dev)
-    t1 = amd.engine.LocalTrainer(f1, C, B, E)
+    t1 = amd.engine.LocalTrainer(f1, C, B, E, split=G)     # same slicing as in the full batch
     t1.upload_perms(seeds.reshape(N, E)[j])
     W1, l1 = t1.run(W0, 0.3, True, 0.01, True, 0.001, False)
     assert torch.equal(W1[0], Wfull[j]) and float(l1[0]) == float(loss[j])
