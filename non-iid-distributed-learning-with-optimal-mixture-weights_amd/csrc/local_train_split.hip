@@ -28,6 +28,9 @@ constexpr int SP_WAVES = 8;
 constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_IDX = 1536;           // E * n_j batch positions staged per client (all epochs)
 constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
+#ifndef SP_STAGGER_CYCLES
+#define SP_STAGGER_CYCLES 0
+#endif
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -178,6 +181,15 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
   SP_STAGE_STORE(0);
   __syncthreads();
 
+  // Stagger: every client runs the same load -> compute -> exchange cycle, so in lockstep
+  // all CUs would burst their next-slice loads into HBM at the same moment and idle it
+  // during compute.  Client slot cs starts (cs % 4) quarter-steps late (wall-clock delay;
+  // speed only, results unaffected) so the chip's load bursts interleave.
+  if (SP_STAGGER_CYCLES > 0 && (cs & 3)) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime() + (unsigned long long)(cs & 3) * SP_STAGGER_CYCLES;
+    while (__builtin_amdgcn_s_memtime() < t_end) __builtin_amdgcn_s_sleep(8);
+  }
+
   double lsum = 0.0;
 #ifdef FS_STAMPS
   unsigned long long stamp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
@@ -221,10 +233,6 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
       for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
         for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][ct * 16 + l16] = acc[rt][ct][i];
-    // next step's slice: issued here so HBM streams during the rest of this step (landed in
-    // LDS after the backward).  Wave 0 holds the poll, whose vmcnt would wait for these
-    // loads, so it issues its share right after the hand-off instead.
-    if (more && w != 0) SP_STAGE_LOAD(st + 1);
     SP_STAMP(1)
     lds_barrier();  // S1: wave partials (and the previous update's norm partials)
     SP_STAMP(2)
@@ -244,6 +252,12 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
     }
     lds_barrier();  // S1b
     SP_STAMP(3)
+    // next step's slice: waves 1-7 issue it now, while wave 0 runs the hand-off, so their
+    // stalls issuing loads into a busy memory pipe overlap the exchange latency (nobody
+    // waits for them before S2); it streams from HBM during the rest of the step and lands
+    // in LDS after the backward.  Wave 0's poll and payload loads would queue behind these
+    // (vmcnt is in order), so wave 0 issues its share after the hand-off.
+    if (more && w != 0) SP_STAGE_LOAD(st + 1);
 
     // ---- hand-off, wave 0 only (its share of the next slice is not in flight yet, so its
     // vmcnt waits cover exactly the hand-off traffic).  Guideline 16, "sc1" form: payload
