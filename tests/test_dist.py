@@ -1,0 +1,84 @@
+"""Multi-rank host logic on CPU (gloo, world size 2): LPT sharding, per-rank RNG pass
+selection, and the partial-fold + all-reduce combination of the aggregate."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+import fedamw_amd
+from fedamw_amd import dist
+
+
+def test_shard_lpt_balances_and_covers():
+    work = np.array([9, 1, 7, 3, 3, 8, 2, 2])
+    shards = dist.shard_lpt(work, 3)
+    allc = np.sort(np.concatenate(shards))
+    np.testing.assert_array_equal(allc, np.arange(len(work)))
+    loads = [work[s].sum() for s in shards]
+    assert max(loads) - min(loads) <= work.max()
+    for s in shards:
+        assert list(s) == sorted(s)           # global order inside a shard
+
+
+def test_client_work_counts_steps():
+    np.testing.assert_array_equal(dist.client_work([32, 33, 1], 2, 32), [2, 4, 2])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        rs = np.random.RandomState(0)
+        N, C, D = 7, 3, 16
+        Ws = rs.normal(size=(N, C, D)).astype(np.float32)
+        ns = rs.randint(10, 100, size=N)
+        p = (ns / ns.sum()).astype(np.float32)
+        shards = dist.shard_lpt(dist.client_work(ns, 2, 32), world)
+        mine = shards[rank]
+        # rank-local ordered fold, then the single all-reduce of the round
+        part = np.zeros((C, D), np.float32)
+        for j in mine:
+            part = (part + p[j] * Ws[j]).astype(np.float32)
+        t = torch.from_numpy(part)
+        dist.allreduce_sum_(t)
+        # every rank draws the same seeds and keeps only its clients' passes
+        torch.manual_seed(5)
+        seeds = torch.empty(2 * N * 2, dtype=torch.int64).random_()[1::2].numpy().reshape(N, 2)
+        g = dist.allgather_rows(torch.from_numpy(seeds[mine]), [len(s) for s in shards])
+        inv = np.argsort(np.concatenate(shards), kind='stable')
+        out[rank] = (t.numpy(), g.numpy()[inv], seeds)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_two_rank_aggregate_and_seed_partition():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rs = np.random.RandomState(0)
+    N, C, D = 7, 3, 16
+    Ws = rs.normal(size=(N, C, D)).astype(np.float32)
+    ns = rs.randint(10, 100, size=N)
+    p = (ns / ns.sum()).astype(np.float32)
+    ref = np.zeros((C, D), np.float32)
+    for j in range(N):
+        ref = (ref + p[j] * Ws[j]).astype(np.float32)
+    for r in range(world):
+        agg, gathered, seeds = out[r]
+        assert np.abs(agg - ref).max() <= 1e-6 * np.abs(ref).max()     # fp32 summation-order noise only
+        np.testing.assert_array_equal(gathered, seeds)                 # shards reassemble the global order
+    np.testing.assert_array_equal(out[0][0], out[1][0])               # identical global model on every rank

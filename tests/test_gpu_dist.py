@@ -1,0 +1,74 @@
+"""Sharded (multi-rank) drop-in on the GPU box: 2 ranks share the one GPU through the
+gloo backend (RCCL needs one GPU per rank; the 8-GPU RCCL run is the driver's), and the
+sharded parallel-client FedAvg/FedProx/FedAMW must match the single-process run within
+fp32 summation-order noise."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem():
+    rs = np.random.RandomState(3)
+    D, C, sizes = 192, 6, [40, 23, 64, 7, 90, 33, 51]
+    Xs = [(np.cos(rs.normal(size=(n, D))) / np.sqrt(D)).astype(np.float32) for n in sizes]
+    ys = [rs.randint(0, C, size=n).astype(np.int64) for n in sizes]
+    Xt = (np.cos(rs.normal(size=(70, D))) / np.sqrt(D)).astype(np.float32)
+    yt = rs.randint(0, C, size=70).astype(np.int64)
+    Xv = (np.cos(rs.normal(size=(45, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=45).astype(np.int64)
+    return D, C, Xs, ys, Xt, yt, Xv, yv
+
+
+def _run(algo):
+    import fedamw_amd
+    from fedamw_amd.functions import tools
+    D, C, Xs, ys, Xt, yt, Xv, yv = _problem()
+    T = torch.from_numpy
+    args = ([T(x) for x in Xs], [T(y) for y in ys], T(Xt), T(yt))
+    stats = {}
+    torch.manual_seed(11)
+    if algo == 'fedamw':
+        vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(T(Xv), T(yv)), batch_size=16, shuffle=True)
+        out = tools.FedAMW(*args, vl, 'classification', C, D, 0.5, 2, 32, False, 0.0, True, 1e-3, 3, 0.05,
+                           clients='parallel', stats=stats, verbose=False)
+    else:
+        out = tools.FedProx(*args, 'classification', C, D, 0.5, 2, 32, algo == 'fedprox', 0.02, True, 1e-3, 3,
+                            clients='parallel', stats=stats, verbose=False)
+    return [o.numpy() for o in out], stats['W_global'].cpu().numpy()
+
+
+def _worker(rank, world, port, algo, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        out[rank] = _run(algo)
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize('algo', ['fedavg', 'fedprox', 'fedamw'])
+def test_sharded_matches_single_process(algo):
+    ref, Wref = _run(algo)
+    mgr = mp.get_context('spawn').Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), algo, out), nprocs=2, join=True)
+    for r in range(2):
+        res, W = out[r]
+        assert np.abs(W - Wref).max() <= 1e-5 * np.abs(Wref).max()
+        np.testing.assert_allclose(res[0], ref[0], atol=1e-5)
+        np.testing.assert_allclose(res[1], ref[1], atol=1e-5)
+        assert np.abs(res[2] - ref[2]).max() <= 100.0 / 70 + 1e-4
