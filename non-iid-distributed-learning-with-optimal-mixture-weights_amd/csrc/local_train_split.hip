@@ -51,7 +51,7 @@ constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
 struct SplitWS {
   unsigned* flags;                     // [N][G] epoch of the last published step
   unsigned* err;                       // [1] nonzero: a partner never arrived (spin bound hit)
-  float* xbuf;                         // [N][2][G][SZ] published partials
+  unsigned long long* xbuf;            // [N][2][G][SZ] published partials: {epoch, value} granules
   unsigned long long* stamps;          // [grid][16] diagnostic build only
   int G;
   int SZ;
@@ -106,8 +106,7 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
   const int steps = E * nbat;
   const float* start = P.W_start;
   float* Wj = P.W_out + (int64_t)j * C * ld;
-  unsigned* myflag = X.flags + (int64_t)cs * G;
-  float* xb = X.xbuf + (int64_t)cs * 2 * G * X.SZ;
+  unsigned long long* xb = X.xbuf + (int64_t)cs * 2 * G * X.SZ;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---- weights (and prox anchor) of this slice into registers ----
@@ -252,51 +251,51 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
     }
     lds_barrier();  // S1b
     SP_STAMP(3)
-    // next step's slice: waves 1-7 issue it now, while wave 0 runs the hand-off, so their
-    // stalls issuing loads into a busy memory pipe overlap the exchange latency (nobody
-    // waits for them before S2); it streams from HBM during the rest of the step and lands
-    // in LDS after the backward.  Wave 0's poll and payload loads would queue behind these
-    // (vmcnt is in order), so wave 0 issues its share after the hand-off.
-    if (more && w != 0) SP_STAGE_LOAD(st + 1);
 
-    // ---- hand-off, wave 0 only (its share of the next slice is not in flight yet, so its
-    // vmcnt waits cover exactly the hand-off traffic).  Guideline 16, "sc1" form: payload
-    // stored write-through (relaxed agent-scope atomics = sc1), drained, then ONE lane
-    // stores the epoch flag; partners poll the flag and read the payload with sc1 loads.
-    float* slot = xb + ((int64_t)par * G) * X.SZ;
+    // ---- hand-off, wave 0 only (the other waves' loads are not in flight yet, and vmcnt is
+    // in order, so wave 0's waits cover exactly the hand-off traffic).  Guideline 16, R2
+    // form: every value travels as one 8-byte {epoch, value} granule written by ONE
+    // relaxed agent-scope (sc1) store -- the data is its own flag; a partner re-reads its
+    // granules with sc1 loads until every tag equals this step's epoch: one round trip
+    // once the data is there, no separate flag, no fences.  Tags are epochs (step + 1) of
+    // this launch; the launcher zeroes the buffer before every launch.
+    unsigned long long* slot = xb + ((int64_t)par * G) * X.SZ;
     if (w == 0) {
+      constexpr int PER = (NZ + 2 + 63) / 64;
       const float* zgf = &zg[0][0];
-      for (int idx = lane; idx < NZ + 2; idx += 64)
-        __hip_atomic_store(slot + (int64_t)g * X.SZ + idx, idx < NZ ? zgf[idx] : nrmg[idx - NZ],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(myflag + g, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) {
-        for (int h = 0; h < G; ++h) {
-          if (h == g) continue;
-          unsigned spins = 0;
-          while (__hip_atomic_load(myflag + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > SP_SPIN_LIMIT) {
-              __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
+      const unsigned long long tag = (unsigned long long)epoch << 32;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int idx = lane + 64 * k;
+        if (idx < NZ + 2) {
+          const float v = idx < NZ ? zgf[idx] : nrmg[idx - NZ];
+          __hip_atomic_store(slot + (int64_t)g * X.SZ + idx, tag | __float_as_uint(v), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      // all partials summed in slice order 0..G-1: identical logits in every partner.
-      // Every partner value is loaded before any is used: one round trip, not one per value.
-      constexpr int PER = (NZ + 2 + 63) / 64;
+      // sum in slice order 0..G-1 (identical logits in every partner); all of a partner's
+      // granules are loaded before any is checked: one round trip per sweep
       float pv[G - 1][PER];
-#pragma unroll
       for (int hh = 0; hh < G - 1; ++hh) {
         const int h = hh < g ? hh : hh + 1;
+        const unsigned long long* src = slot + (int64_t)h * X.SZ;
+        unsigned spins = 0;
+        for (;;) {
+          bool ok = true;
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-          const int idx = lane + 64 * k;
-          pv[hh][k] = idx < NZ + 2 ? __hip_atomic_load(slot + (int64_t)h * X.SZ + idx, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0.f;
+          for (int k = 0; k < PER; ++k) {
+            const int idx = lane + 64 * k;
+            unsigned long long x = tag;
+            if (idx < NZ + 2) x = __hip_atomic_load(src + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pv[hh][k] = __uint_as_float((unsigned)x);
+            ok &= (x >> 32) == (unsigned long long)epoch;
+          }
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > SP_SPIN_LIMIT) {
+            if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
         }
       }
       float* zf = &zsum[0][0];
@@ -312,7 +311,6 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
           else nrm[idx - NZ] = v;                // ||W - W_a||^2, ||W||^2 at the start of this step
         }
       }
-      if (more) SP_STAGE_LOAD(st + 1);
     }
     SP_STAMP(4)
     lds_barrier();  // S2: summed logits and norms
@@ -341,6 +339,14 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
     cep = wave_sum(cep);
     if (lane == 0) wce[w] = cep;
     lds_barrier();  // S3: g, CE partials
+    // next step's slice, issued around the backward so it streams behind the backward MFMAs
+    // and lands in LDS after S4 (issuing it during the hand-off slowed the hand-off's own
+    // round trips, which queue behind it in the CU's memory pipe).  Issuing 16 KB per wave
+    // stalls the issuing wave on the memory pipe, so the two waves of a SIMD are staggered:
+    // waves 4-7 issue first and then compute, waves 0-3 compute first and then issue, and
+    // each SIMD's MFMA pipe always has one wave feeding it.
+    const bool load_first = w >= SP_WAVES / 2;
+    if (more && load_first) SP_STAGE_LOAD(st + 1);
     SP_STAMP(6)
     const float pn2 = nrm[0], wn2 = nrm[1];
     if (g == 0 && tid == 0 && e == E - 1) {
@@ -396,6 +402,7 @@ __global__ __launch_bounds__(SP_THREADS) void local_train_split_kernel(LTParams 
         }
       }
     }
+    if (more && !load_first) SP_STAGE_LOAD(st + 1);
     npn = wave_sum(npn);
     nwn = wave_sum(nwn);
     if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
@@ -443,7 +450,7 @@ constexpr size_t SP_STATIC_LDS = 8 * 32 * 16 * 4 + 2 * 32 * 16 * 4 + SP_IDX * 5 
 
 static int64_t split_ws_bytes(int N, int G, int RT) {
   const int SZ = RT * 16 * 16 + 4;
-  return 256 + (int64_t)N * G * 4 + (int64_t)N * 2 * G * SZ * 4;
+  return 256 + ((int64_t)N * G * 4 + 255) / 256 * 256 + (int64_t)N * 2 * G * SZ * 8;
 }
 
 template <int RT, int G, int TPW, bool PROX>
@@ -476,15 +483,16 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   SplitWS X;
   X.err = reinterpret_cast<unsigned*>(base);
   X.flags = reinterpret_cast<unsigned*>(base + 256);
-  X.xbuf = reinterpret_cast<float*>(base + 256 + ((int64_t)P.N * G * 4 + 255) / 256 * 256);
+  X.xbuf = reinterpret_cast<unsigned long long*>(base + 256 + ((int64_t)P.N * G * 4 + 255) / 256 * 256);
   X.G = G;
   X.SZ = RT * 16 * 16 + 4;
   X.stamps = nullptr;
 #ifdef FS_STAMPS
   X.stamps = reinterpret_cast<unsigned long long*>(base + ws_bytes - (int64_t)P.N * G * 16 * 8);
 #endif
-  // flags, error word: zeroed on the stream before every launch (epochs restart at 1)
-  hipError_t e = hipMemsetAsync(base, 0, 256 + (size_t)P.N * G * 4, st);
+  // error word, flags and granule tags: zeroed on the stream before every launch (epochs
+  // restart at 1, so no granule of an earlier launch can carry a matching tag)
+  hipError_t e = hipMemsetAsync(base, 0, (size_t)split_ws_bytes(P.N, G, RT), st);
   if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
 #define FS_SPLIT_CASE(rt, g, tp) \
   if (RT == rt && G == g && tpw <= tp) { launch_split_t<rt, g, tp>(P, X, lds, st); return FS_OK; }
