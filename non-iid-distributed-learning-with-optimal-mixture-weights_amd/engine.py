@@ -164,19 +164,22 @@ class LocalTrainer:
         the permutations are replayed on the GPU into shuffle slot ``slot``."""
         self.shuffler.prepare(seeds, slot, stream)
 
-    def run(self, W_start, lr, prox, mu, reg, lam, chained, slot=0):
+    def run(self, W_start, lr, prox, mu, reg, lam, chained, slot=0, loss_out=None):
+        """Launch local training of every client; ``loss_out`` (float64 [N], default the
+        trainer's own buffer) receives the last-epoch losses."""
         f = self.f
         L = _lib.lib()
+        loss = self.loss if loss_out is None else loss_out
         perms = self.shuffler.acquire(slot)
         _lib.check(L.fs_local_train(_lib.ptr(f.phi), f.ld, _lib.ptr(f.row_off_dev), _lib.ptr(f.labels),
                                     _lib.ptr(perms), None if chained else _lib.ptr(self.order),
                                     self.N, self.C, self.B, self.E, float(lr), float(mu), int(bool(prox)),
                                     float(lam), int(bool(reg)), int(bool(chained)), _lib.ptr(W_start),
-                                    _lib.ptr(self.W_out), _lib.ptr(self.loss), self.G, _lib.ptr(self.ws),
+                                    _lib.ptr(self.W_out), _lib.ptr(loss), self.G, _lib.ptr(self.ws),
                                     0 if self.ws is None else self.ws.numel(), _lib.stream_ptr()),
                    'fs_local_train')
         self.shuffler.release(slot)
-        return self.W_out, self.loss
+        return self.W_out, loss
 
 
 class Aggregator:

@@ -162,11 +162,10 @@ class Federation:
         self.lr = update_learning_rate(t, self.lr, self.R)
         if self.on_local_train:
             self.on_local_train[0]()
-        W_out, loss = self.trainer.run(self.W_g, self.lr, self.prox, self.mu, self.reg, self.lam, self.chained,
-                                       slot=t % 2)
+        W_out, _ = self.trainer.run(self.W_g, self.lr, self.prox, self.mu, self.reg, self.lam, self.chained,
+                                    slot=t % 2, loss_out=self.loss_hist[t])
         if self.on_local_train:
             self.on_local_train[1]()
-        self.loss_hist[t].copy_(loss)
         if self.mixture is not None:
             self.p_hist[t].copy_(self.mixture.p)
             W_all = W_out
