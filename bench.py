@@ -56,6 +56,7 @@ def parse():
     ap.add_argument('--shape', default='a9a', choices=['a9a', 'covtype'])
     ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--host-shuffle', action='store_true', help='replay shuffles on host threads, not the GPU')
     return ap.parse_args()
 
 
@@ -134,7 +135,7 @@ def main():
     torch.manual_seed(100)
     fed = tools.Federation(args.algo, Xs, ys, d['X_test'], d['y_test'], vl, 'classification', args.C, args.D, lr,
                            E, B, args.algo == 'fedprox', mu, args.algo == 'fedamw', 1e-5, R, 1e-3,
-                           'parallel', verbose=False)
+                           'parallel', verbose=False, shuffle_device=not args.host_shuffle)
     assert len(fed.mine) == N_loc
     ev_pairs = []
 

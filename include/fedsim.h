@@ -34,7 +34,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 2
+#define FS_ABI_VERSION 3
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -134,6 +134,68 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
 int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                  int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
                  int* d_first, void* stream);
+
+
+/* ------------------------------------------------------------------------- *
+ * Round plan: the native round driver.  One fs_plan_round call enqueues the
+ * launches of one round of the reference's loop (tools.py:337-352 FedAvg,
+ * 364-379 FedProx; the train / aggregate / evaluate phases of FedAMW, 427-462):
+ *   FS_PHASE_TRAIN      fs_local_train over all N clients with the shuffles of
+ *                       round t; losses to d_loss_hist[t*N .. t*N+N)
+ *   FS_PHASE_AGGREGATE  fs_aggregate(W_out, p) -> d_W_g  (p = d_p, or the override)
+ *   FS_PHASE_EVAL       fs_eval(d_W_g) -> d_eval_hist[2t], [2t+1]
+ * fs_plan_shuffle(plan, seeds, t) replays round t's N*E training shuffles
+ * (DataLoader passes of tools.py:179, client-major / epoch-minor seeds) into slot
+ * t % 2 on the plan's side stream -- on the GPU (fs_randperm_device, default) or on
+ * the plan's host thread pool plus an async upload; call it for round t+1 after
+ * enqueueing round t so it overlaps the GPU.
+ * The plan owns its shuffle buffers, copy stream and events; every other pointer
+ * is borrowed and must outlive the plan.
+ * ------------------------------------------------------------------------- */
+#define FS_PHASE_TRAIN 1
+#define FS_PHASE_AGGREGATE 2
+#define FS_PHASE_EVAL 4
+
+typedef struct fs_plan fs_plan;
+
+typedef struct fs_plan_desc {
+  /* local training (see fs_local_train) */
+  const float* d_phi;
+  int64_t ld;
+  const int64_t* d_row_off;
+  const int32_t* d_labels;
+  const int32_t* d_order;
+  const int64_t* h_n;          /* [N] rows per client (host) */
+  int N, C, B, E;
+  int G;                       /* from fs_local_train_plan (1 when chained) */
+  void* d_ws;
+  int64_t ws_bytes;
+  int chained, prox, reg;
+  float mu, lam;
+  float* d_W_g;                /* [C][ld] round-start model; the aggregate is written here */
+  float* d_W_out;              /* [N][C][ld] */
+  double* d_loss_hist;         /* [R][N] */
+  /* aggregation (see fs_aggregate) */
+  const float* d_p;            /* [N] default mixture weights (may be NULL) */
+  float* d_agg_ws;
+  int64_t agg_ws_floats;
+  int agg_chunks;
+  /* evaluation (see fs_eval; may be NULL when FS_PHASE_EVAL is never used) */
+  const float* d_phi_t;
+  const int32_t* d_labels_t;
+  int n_t;
+  double* d_eval_ws;
+  double* d_eval_hist;         /* [R][2] */
+  int shuffle_device;          /* 1: replay shuffles with fs_randperm_device on the plan's side
+                                  stream; 0: on the plan's host thread pool + async upload */
+  int host_threads;            /* host replay threads; <= 0: min(16, hardware) */
+} fs_plan_desc;
+
+int64_t fs_plan_desc_size(void);   /* sizeof(fs_plan_desc), for binding-layout checks */
+int fs_plan_create(const fs_plan_desc* desc, fs_plan** out);
+int fs_plan_destroy(fs_plan* plan);
+int fs_plan_shuffle(fs_plan* plan, const int64_t* h_seeds, int t);
+int fs_plan_round(fs_plan* plan, int t, float lr, int phases, const float* d_p_override, void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,10 +35,32 @@ _SIGS = {
     'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p]),
+    'fs_plan_desc_size': (C.c_int64, []),
+    'fs_plan_create': (C.c_int, [C.c_void_p, C.c_void_p]),
+    'fs_plan_destroy': (C.c_int, [C.c_void_p]),
+    'fs_plan_shuffle': (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    'fs_plan_round': (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 2
+ABI_VERSION = 3
+
+PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
+
+
+class PlanDesc(C.Structure):
+    """fs_plan_desc (include/fedsim.h), field for field."""
+    _fields_ = [
+        ('d_phi', C.c_void_p), ('ld', C.c_int64), ('d_row_off', C.c_void_p), ('d_labels', C.c_void_p),
+        ('d_order', C.c_void_p), ('h_n', C.c_void_p),
+        ('N', C.c_int), ('C', C.c_int), ('B', C.c_int), ('E', C.c_int), ('G', C.c_int),
+        ('d_ws', C.c_void_p), ('ws_bytes', C.c_int64),
+        ('chained', C.c_int), ('prox', C.c_int), ('reg', C.c_int), ('mu', C.c_float), ('lam', C.c_float),
+        ('d_W_g', C.c_void_p), ('d_W_out', C.c_void_p), ('d_loss_hist', C.c_void_p),
+        ('d_p', C.c_void_p), ('d_agg_ws', C.c_void_p), ('agg_ws_floats', C.c_int64), ('agg_chunks', C.c_int),
+        ('d_phi_t', C.c_void_p), ('d_labels_t', C.c_void_p), ('n_t', C.c_int), ('d_eval_ws', C.c_void_p),
+        ('d_eval_hist', C.c_void_p), ('shuffle_device', C.c_int), ('host_threads', C.c_int),
+    ]
 
 _lib = None
 
@@ -64,6 +86,9 @@ def lib():
             f.argtypes = args
         if h.fs_abi_version() != ABI_VERSION:
             raise FedsimError('libfedsim.so ABI %d != %d' % (h.fs_abi_version(), ABI_VERSION))
+        if h.fs_plan_desc_size() != C.sizeof(PlanDesc):
+            raise FedsimError('fs_plan_desc layout mismatch (%d != %d bytes)' % (h.fs_plan_desc_size(),
+                                                                                  C.sizeof(PlanDesc)))
         _lib = h
     return _lib
 

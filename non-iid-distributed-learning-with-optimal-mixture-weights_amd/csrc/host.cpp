@@ -11,12 +11,12 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
-#include <random>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/fedsim.h"
+#include "mt_replay.h"
 
 namespace fs {
 
@@ -27,15 +27,6 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
-}
-
-static void randperm_one(uint64_t seed, int64_t n, int32_t* out) {
-  for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)i;
-  std::mt19937 g((uint32_t)seed);
-  for (int64_t i = 0; i + 1 < n; ++i) {
-    const int64_t z = (int64_t)(g() % (uint32_t)(n - i));
-    std::swap(out[i], out[i + z]);
-  }
 }
 
 }  // namespace fs
@@ -54,7 +45,7 @@ extern "C" int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, con
   int64_t total = 0;
   for (int64_t i = 0; i < npasses; ++i) total += h_n[i];
   if (nthreads == 1 || npasses <= 1 || total < (1 << 15)) {
-    for (int64_t i = 0; i < npasses; ++i) fs::randperm_one((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
+    for (int64_t i = 0; i < npasses; ++i) fs::replay_randperm((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
     return FS_OK;
   }
   nthreads = (int)std::min<int64_t>(nthreads, npasses);
@@ -63,7 +54,7 @@ extern "C" int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, con
     for (;;) {
       const int64_t i = next.fetch_add(1);
       if (i >= npasses) return;
-      fs::randperm_one((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
+      fs::replay_randperm((uint64_t)h_seeds[i], h_n[i], h_out + h_off[i]);
     }
   };
   std::vector<std::thread> pool;

@@ -1,0 +1,358 @@
+// fs_plan -- the native round driver.
+//
+// One call enqueues the launches of one federated round of FedAvg / FedProx (and the
+// local-training / aggregation / evaluation phases of FedAMW), replacing the per-round
+// Python work of the reference's round loop (/root/reference/functions/tools.py:337-352,
+// 364-379, 427-462):
+//   TRAIN      fs_local_train over every client (train_loop, tools.py:340-343), losses
+//              written straight into the [R][N] history
+//   AGGREGATE  fs_aggregate: W_g = sum_j p_j W_j (tools.py:345-350)
+//   EVAL       fs_eval of W_g on the test set into the [R][2] history (tools.py:351)
+// The DataLoader shuffles of a round (tools.py:179, one RandomSampler permutation per
+// client and epoch) are replayed bit-exactly (MT19937 + forward Fisher-Yates) into one of
+// two slots on the plan's own side stream, so round t+1's shuffles are produced while
+// round t trains:
+//   shuffle_device = 1  fs_randperm_device (one wave per pass) after an async upload of
+//                       the seeds from pinned memory -- a few hundred waves beside the
+//                       local-training grid, no host work;
+//   shuffle_device = 0  a persistent pool of host threads (as fs_randperm_batch) driven by
+//                       a coordinator thread, then one async upload of the permutations.
+// Events order the slots: a slot is rewritten only after the local training that
+// consumed its previous contents, and a local training waits for its slot.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <deque>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+#include "mt_replay.h"
+
+namespace fs {
+
+// Persistent worker pool: run(n, fn) calls fn(i) for i in [0, n) on all workers + the caller.
+class Pool {
+ public:
+  explicit Pool(int nthreads) {
+    for (int t = 1; t < nthreads; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(int64_t n, const std::function<void(int64_t)>& fn) {
+    if (th_.empty() || n <= 1) {
+      for (int64_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      busy_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int64_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--busy_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int64_t)>* fn_ = nullptr;
+  int64_t n_ = 0;
+  std::atomic<int64_t> next_{0};
+  int busy_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace fs
+
+struct fs_plan {
+  fs_plan_desc d;
+  std::vector<int64_t> n, off;         // per pass (j*E + e): rows, offset into the shuffle buffer
+  int64_t perm_len = 0;                // E * rows
+  int32_t* h_perm[2] = {nullptr, nullptr};   // pinned (host replay)
+  int32_t* d_perm[2] = {nullptr, nullptr};
+  int64_t* h_seed[2] = {nullptr, nullptr};   // pinned (device replay)
+  int64_t* d_seed[2] = {nullptr, nullptr};
+  int64_t* d_pass = nullptr;                 // [2][P]: rows, offset of every pass (device replay)
+  int64_t max_n = 0;
+  hipStream_t copy = nullptr;
+  hipEvent_t uploaded[2] = {nullptr, nullptr};
+  hipEvent_t consumed[2] = {nullptr, nullptr};
+  bool up_pending[2] = {false, false};
+  bool cons_recorded[2] = {false, false};
+  int slot_round[2] = {-1, -1};       // round whose shuffles slot s holds (set by the coordinator)
+  int job_status = FS_OK;
+  std::string job_error;
+  fs::Pool* pool = nullptr;
+  // coordinator: shuffle jobs (round, seeds) in order
+  std::thread coord;
+  std::mutex m;
+  std::condition_variable cv, done;
+  std::deque<std::pair<int, std::vector<int64_t>>> jobs;
+  bool stop = false;
+};
+
+using namespace fs;
+
+static int hip_fail(const char* what, hipError_t e) {
+  return fail(FS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define FS_HIP(call, what)                          \
+  do {                                              \
+    hipError_t e_ = (call);                         \
+    if (e_ != hipSuccess) return hip_fail(what, e_); \
+  } while (0)
+
+extern "C" int64_t fs_plan_desc_size(void) { return (int64_t)sizeof(fs_plan_desc); }
+
+static int run_shuffle_job(fs_plan* p, const int64_t* h_seeds, int t);
+
+static void coordinator(fs_plan* p) {
+  for (;;) {
+    std::pair<int, std::vector<int64_t>> job;
+    {
+      std::unique_lock<std::mutex> lk(p->m);
+      p->cv.wait(lk, [p] { return p->stop || !p->jobs.empty(); });
+      if (p->jobs.empty()) return;
+      job = std::move(p->jobs.front());
+    }
+    const int rc = run_shuffle_job(p, job.second.data(), job.first);
+    std::lock_guard<std::mutex> lk(p->m);
+    p->jobs.pop_front();
+    if (rc != FS_OK && p->job_status == FS_OK) {
+      p->job_status = rc;
+      p->job_error = fs_last_error();
+    }
+    p->done.notify_all();
+  }
+}
+
+extern "C" int fs_plan_destroy(fs_plan* p) {
+  if (!p) return FS_OK;
+  if (p->coord.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(p->m);
+      p->stop = true;
+    }
+    p->cv.notify_all();
+    p->coord.join();
+  }
+  if (p->copy) (void)hipStreamSynchronize(p->copy);
+  for (int s = 0; s < 2; ++s) {
+    if (p->h_perm[s]) (void)hipHostFree(p->h_perm[s]);
+    if (p->d_perm[s]) (void)hipFree(p->d_perm[s]);
+    if (p->h_seed[s]) (void)hipHostFree(p->h_seed[s]);
+    if (p->d_seed[s]) (void)hipFree(p->d_seed[s]);
+    if (p->uploaded[s]) (void)hipEventDestroy(p->uploaded[s]);
+    if (p->consumed[s]) (void)hipEventDestroy(p->consumed[s]);
+  }
+  if (p->d_pass) (void)hipFree(p->d_pass);
+  if (p->copy) (void)hipStreamDestroy(p->copy);
+  delete p->pool;
+  delete p;
+  return FS_OK;
+}
+
+extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
+  FS_REQUIRE(desc && out, "null pointer");
+  const fs_plan_desc& d = *desc;
+  FS_REQUIRE(d.N >= 1 && d.E >= 0 && d.C >= 1 && d.ld >= 64 && d.ld % 64 == 0, "bad sizes");
+  FS_REQUIRE(d.h_n && d.d_phi && d.d_row_off && d.d_labels && d.d_W_g && d.d_W_out && d.d_loss_hist,
+             "null pointer");
+  *out = nullptr;
+  fs_plan* p = new fs_plan();
+  p->d = d;
+  int64_t rows = 0;
+  for (int j = 0; j < d.N; ++j) {
+    if (d.h_n[j] < 0) {
+      delete p;
+      return fail(FS_EINVAL, "fs_plan_create: negative client size");
+    }
+    for (int e = 0; e < d.E; ++e) {
+      p->n.push_back(d.h_n[j]);
+      p->off.push_back((int64_t)d.E * rows + (int64_t)e * d.h_n[j]);
+    }
+    rows += d.h_n[j];
+  }
+  p->perm_len = std::max<int64_t>(1, (int64_t)d.E * rows);
+  const int64_t P = (int64_t)p->n.size();
+  for (int64_t v : p->n) p->max_n = std::max(p->max_n, v);
+  hipError_t e = hipSuccess;
+  for (int s = 0; s < 2 && e == hipSuccess; ++s) {
+    if (d.shuffle_device) {
+      e = hipHostMalloc(reinterpret_cast<void**>(&p->h_seed[s]), sizeof(int64_t) * std::max<int64_t>(1, P),
+                        hipHostMallocDefault);
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_seed[s]), sizeof(int64_t) * std::max<int64_t>(1, P));
+    } else {
+      e = hipHostMalloc(reinterpret_cast<void**>(&p->h_perm[s]), sizeof(int32_t) * p->perm_len, hipHostMallocDefault);
+    }
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_perm[s]), sizeof(int32_t) * p->perm_len);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->uploaded[s], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->consumed[s], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
+  if (e == hipSuccess && d.shuffle_device && P > 0) {
+    std::vector<int64_t> h(2 * P);
+    std::copy(p->n.begin(), p->n.end(), h.begin());
+    std::copy(p->off.begin(), p->off.end(), h.begin() + P);
+    e = hipMalloc(reinterpret_cast<void**>(&p->d_pass), sizeof(int64_t) * 2 * P);
+    if (e == hipSuccess) e = hipMemcpy(p->d_pass, h.data(), sizeof(int64_t) * 2 * P, hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    fs_plan_destroy(p);
+    return hip_fail("fs_plan_create", e);
+  }
+  if (!d.shuffle_device) {
+    const int nthreads =
+        d.host_threads > 0 ? d.host_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    p->pool = new Pool(nthreads);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    p->coord = std::thread([p, dev] {
+      (void)hipSetDevice(dev);
+      coordinator(p);
+    });
+  }
+  *out = p;
+  return FS_OK;
+}
+
+// Device replay: upload the seeds and launch fs_randperm_device on the side stream.
+static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
+  const int s = t & 1;
+  const int64_t P = (int64_t)p->n.size();
+  if (p->up_pending[s]) FS_HIP(hipEventSynchronize(p->uploaded[s]), "fs_plan_shuffle");   // pinned seeds free
+  std::memcpy(p->h_seed[s], h_seeds, sizeof(int64_t) * P);
+  if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
+  FS_HIP(hipMemcpyAsync(p->d_seed[s], p->h_seed[s], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
+         "fs_plan_shuffle");
+  const int rc = fs_randperm_device(p->d_seed[s], p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], p->copy);
+  if (rc != FS_OK) return rc;
+  FS_HIP(hipEventRecord(p->uploaded[s], p->copy), "fs_plan_shuffle");
+  p->up_pending[s] = true;
+  p->slot_round[s] = t;
+  return FS_OK;
+}
+
+// Prepare round t's shuffles: device replay is enqueued here; a host replay job is queued
+// for the coordinator thread and this returns at once.
+extern "C" int fs_plan_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
+  FS_REQUIRE(p && (h_seeds || p->n.empty()) && t >= 0, "bad arguments");
+  if (p->d.shuffle_device) {
+    if (p->n.empty()) {
+      p->slot_round[t & 1] = t;
+      return FS_OK;
+    }
+    return device_shuffle(p, h_seeds, t);
+  }
+  {
+    std::lock_guard<std::mutex> lk(p->m);
+    if (p->job_status != FS_OK) return fail(p->job_status, p->job_error);
+    p->jobs.emplace_back(t, std::vector<int64_t>(h_seeds, h_seeds + p->n.size()));
+  }
+  p->cv.notify_all();
+  return FS_OK;
+}
+
+static int run_shuffle_job(fs_plan* p, const int64_t* h_seeds, int t) {
+  const int s = t & 1;
+  if (p->up_pending[s]) FS_HIP(hipEventSynchronize(p->uploaded[s]), "fs_plan_shuffle");   // pinned slot free
+  int32_t* out = p->h_perm[s];
+  const std::function<void(int64_t)> one = [&](int64_t i) {
+    replay_randperm((uint64_t)h_seeds[i], p->n[i], out + p->off[i]);
+  };
+  p->pool->run((int64_t)p->n.size(), one);
+  // the device slot is rewritten only after the local training that read it has finished
+  if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
+  FS_HIP(hipMemcpyAsync(p->d_perm[s], out, sizeof(int32_t) * p->perm_len, hipMemcpyHostToDevice, p->copy),
+         "fs_plan_shuffle");
+  FS_HIP(hipEventRecord(p->uploaded[s], p->copy), "fs_plan_shuffle");
+  p->up_pending[s] = true;
+  std::lock_guard<std::mutex> lk(p->m);
+  p->slot_round[s] = t;
+  return FS_OK;
+}
+
+extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const float* d_p_override, void* stream) {
+  FS_REQUIRE(p && t >= 0, "bad arguments");
+  const fs_plan_desc& d = p->d;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int s = t & 1;
+  if (phases & FS_PHASE_TRAIN) {
+    {
+      // wait for this round's shuffle job (normally finished long ago)
+      std::unique_lock<std::mutex> lk(p->m);
+      p->done.wait(lk, [&] {
+        if (p->job_status != FS_OK || p->slot_round[s] == t) return true;
+        for (auto& j : p->jobs) if (j.first == t) return false;
+        return true;                               // never queued
+      });
+      if (p->job_status != FS_OK) return fail(p->job_status, p->job_error);
+      if (p->slot_round[s] != t) return fail(FS_EINVAL, "fs_plan_round: shuffles of this round were not prepared");
+    }
+    FS_HIP(hipStreamWaitEvent(st, p->uploaded[s], 0), "fs_plan_round");
+    const int rc = fs_local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[s], d.d_order, d.N, d.C, d.B,
+                                  d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g, d.d_W_out,
+                                  d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, stream);
+    if (rc != FS_OK) return rc;
+    FS_HIP(hipEventRecord(p->consumed[s], st), "fs_plan_round");
+    p->cons_recorded[s] = true;
+  }
+  if (phases & FS_PHASE_AGGREGATE) {
+    const float* pw = d_p_override ? d_p_override : d.d_p;
+    FS_REQUIRE(pw, "no mixture weights");
+    const int64_t len = (int64_t)d.C * d.ld;
+    const int rc = fs_aggregate(d.d_W_out, len, pw, d.N, len, d.d_W_g, d.d_agg_ws, d.agg_ws_floats, d.agg_chunks,
+                                stream);
+    if (rc != FS_OK) return rc;
+  }
+  if (phases & FS_PHASE_EVAL) {
+    FS_REQUIRE(d.d_phi_t && d.d_labels_t && d.d_eval_hist && d.d_eval_ws, "no test set");
+    const int rc = fs_eval(d.d_phi_t, d.ld, d.d_labels_t, d.n_t, d.d_W_g, d.C, d.d_eval_hist + 2 * (int64_t)t,
+                           d.d_eval_ws, stream);
+    if (rc != FS_OK) return rc;
+  }
+  return FS_OK;
+}

@@ -136,7 +136,7 @@ class LocalTrainer:
         self.pass_n = np.repeat(ns, self.E)
         self.pass_off = (np.repeat(self.E * feats.row_off[:-1], self.E)
                          + np.tile(np.arange(self.E), N) * np.repeat(ns, self.E)).astype(np.int64)
-        self.shuffler = Shuffler(self.pass_n, self.pass_off, self.E * feats.rows, dev)
+        self._shuffler = None
         steps = self.E * ((ns + self.B - 1) // self.B)
         order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
         self.order = torch.from_numpy(order).to(dev)
@@ -151,6 +151,13 @@ class LocalTrainer:
                 wsb.value = max(int(wsb.value), 1 << 20)
         self.G = int(g.value)
         self.ws = torch.zeros(max(256, int(wsb.value)), dtype=torch.uint8, device=dev) if self.G > 1 else None
+
+    @property
+    def shuffler(self):
+        """GPU shuffle replay for direct ``run`` calls (the round plan owns its own slots)."""
+        if self._shuffler is None:
+            self._shuffler = Shuffler(self.pass_n, self.pass_off, self.E * self.f.rows, self.f.device)
+        return self._shuffler
 
     def check_errors(self):
         """Raise if a split-client launch reported a broken hand-off (synchronises)."""
@@ -180,6 +187,61 @@ class LocalTrainer:
                    'fs_local_train')
         self.shuffler.release(slot)
         return self.W_out, loss
+
+
+class RoundPlan:
+    """fs_plan: the native round driver (csrc/round.hip).  One ``round`` call enqueues a
+    round's local training / aggregation / evaluation; ``shuffle`` replays a round's
+    training shuffles into a slot on the plan's side stream (GPU replay by default,
+    ``shuffle_device=False``: host thread pool + async upload).
+    Borrows every device buffer from the objects passed in (they must outlive it)."""
+
+    def __init__(self, trainer, W_g, loss_hist, p=None, aggregator=None, evaluator=None, eval_hist=None,
+                 prox=False, mu=0.0, reg=False, lam=0.0, chained=False, shuffle_device=True, host_threads=0):
+        import ctypes
+        f = trainer.f
+        self._keep = [trainer, W_g, loss_hist, p, aggregator, evaluator, eval_hist]
+        self._h_n = np.ascontiguousarray(f.ns, dtype=np.int64)
+        d = _lib.PlanDesc()
+        d.d_phi, d.ld, d.d_row_off, d.d_labels = f.phi.data_ptr(), f.ld, f.row_off_dev.data_ptr(), f.labels.data_ptr()
+        d.d_order = None if chained else trainer.order.data_ptr()
+        d.h_n = self._h_n.ctypes.data
+        d.N, d.C, d.B, d.E, d.G = trainer.N, trainer.C, trainer.B, trainer.E, trainer.G
+        d.d_ws = None if trainer.ws is None else trainer.ws.data_ptr()
+        d.ws_bytes = 0 if trainer.ws is None else trainer.ws.numel()
+        d.chained, d.prox, d.reg = int(bool(chained)), int(bool(prox)), int(bool(reg))
+        d.mu, d.lam = float(mu), float(lam)
+        d.d_W_g, d.d_W_out, d.d_loss_hist = W_g.data_ptr(), trainer.W_out.data_ptr(), loss_hist.data_ptr()
+        d.d_p = None if p is None else p.data_ptr()
+        if aggregator is not None:
+            d.d_agg_ws, d.agg_ws_floats, d.agg_chunks = aggregator.ws.data_ptr(), aggregator.ws.numel(), \
+                int(aggregator.chunks)
+        if evaluator is not None:
+            d.d_phi_t, d.d_labels_t, d.n_t = evaluator.f.phi.data_ptr(), evaluator.f.labels.data_ptr(), evaluator.n
+            d.d_eval_ws, d.d_eval_hist = evaluator.ws.data_ptr(), eval_hist.data_ptr()
+        d.shuffle_device = int(bool(shuffle_device))
+        d.host_threads = int(host_threads)
+        self._desc = d
+        self._h = ctypes.c_void_p()
+        _lib.check(_lib.lib().fs_plan_create(ctypes.byref(d), ctypes.byref(self._h)), 'fs_plan_create')
+        self.npasses = int(trainer.N * trainer.E)
+
+    def shuffle(self, seeds, t):
+        """seeds: [N*E] sampler seeds of round t's training passes (client-major)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.int64)
+        assert seeds.shape == (self.npasses,)
+        _lib.check(_lib.lib().fs_plan_shuffle(self._h, seeds.ctypes.data, int(t)), 'fs_plan_shuffle')
+
+    def round(self, t, lr, phases, p_override=None):
+        _lib.check(_lib.lib().fs_plan_round(self._h, int(t), float(lr), int(phases),
+                                            None if p_override is None else _lib.ptr(p_override),
+                                            _lib.stream_ptr()), 'fs_plan_round')
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.fs_plan_destroy(h)
+            self._h = None
 
 
 class Aggregator:

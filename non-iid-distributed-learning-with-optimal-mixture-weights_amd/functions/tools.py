@@ -34,6 +34,7 @@ import numpy as np
 import torch
 
 from .. import dist, engine, rng
+from .. import _lib
 from .._lib import FedsimError
 
 __all__ = ['FedAvg', 'FedProx', 'FedAMW', 'Federation', 'update_learning_rate', 'init_weights']
@@ -86,7 +87,8 @@ class Federation:
     rounds one at a time through the same code path as the drop-ins)."""
 
     def __init__(self, algo, X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
-                 batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=None, verbose=True):
+                 batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=None, verbose=True,
+                 shuffle_device=True):
         _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round)
         if clients not in ('sequential', 'parallel'):
             raise ValueError("clients must be 'sequential' or 'parallel'")
@@ -136,51 +138,61 @@ class Federation:
         self.eval_hist = torch.empty(R, 2, dtype=torch.float64, device=dev)
         self.W_hist = torch.empty(R, C, ld, device=dev) if (stats is not None and stats.get('trace')) else None
         self.n_val_pass = R if algo == 'fedamw' else 0
-        self.side = torch.cuda.Stream(device=dev)    # shuffles of round t+1 are replayed here during round t
+        self.side = torch.cuda.Stream(device=dev)    # FedAMW validation shuffles of round t+1 run here
+        # the native round driver (csrc/round.hip): one call per round phase, training shuffles
+        # replayed into a double-buffered slot on its side stream
+        self.plan = engine.RoundPlan(self.trainer, self.W_g, self.loss_hist, p=self.p_mine,
+                                     aggregator=self.agg if self.mixture is None else None,
+                                     evaluator=self.evaluator, eval_hist=self.eval_hist, prox=prox, mu=mu,
+                                     reg=lambda_reg_if, lam=lambda_reg, chained=self.chained,
+                                     shuffle_device=shuffle_device)
         self.t = 0
         self.on_local_train = None      # optional (before, after) hooks around the local-training launch
 
     def _prepare(self, t):
         """Draw round t's shuffle seeds (torch's global CPU generator, in the reference's
-        order: train passes client-major, then validation passes, then the test pass) and
-        enqueue their GPU replay on the side stream into slot t % 2."""
+        order: train passes client-major, then validation passes, then the test pass), replay
+        the training shuffles into the plan's slot t % 2 (on its side stream) and enqueue the validation shuffles (FedAMW) on the side stream."""
         N, E = self.N, self.E
         seeds = rng.draw_pass_seeds(N * E + self.n_val_pass + 1)
-        self.trainer.upload_perms(seeds[:N * E].reshape(N, E)[self.mine].reshape(-1), t % 2, self.side)
+        self.plan.shuffle(seeds[:N * E].reshape(N, E)[self.mine].reshape(-1), t)
         if self.mixture is not None:
             self.mixture.prepare(seeds[N * E:N * E + self.n_val_pass], t % 2, self.side)
 
     def round(self):
-        """Run round t (tools.py:337-352 / 364-379 / 427-462) -- all launches async.  The draw
-        pattern is data-independent, so drawing round t+1's seeds during round t leaves the
-        generator exactly where the reference leaves it after each call."""
+        """Run round t (tools.py:337-352 / 364-379 / 427-462) -- all launches async.  Round
+        t+1's seeds are drawn (and its shuffles replayed) after round t is
+        enqueued, so the host work overlaps the GPU; the draw pattern is data-independent,
+        so this leaves the generator exactly where the reference leaves it after each call."""
         t = self.t
         if t == 0:
             self._prepare(0)
-        if t + 1 < self.R:
-            self._prepare(t + 1)
         self.lr = update_learning_rate(t, self.lr, self.R)
+        P = _lib.PHASE_TRAIN, _lib.PHASE_AGGREGATE, _lib.PHASE_EVAL
         if self.on_local_train:
             self.on_local_train[0]()
-        W_out, _ = self.trainer.run(self.W_g, self.lr, self.prox, self.mu, self.reg, self.lam, self.chained,
-                                    slot=t % 2, loss_out=self.loss_hist[t])
+        self.plan.round(t, self.lr, P[0])
         if self.on_local_train:
             self.on_local_train[1]()
         if self.mixture is not None:
             self.p_hist[t].copy_(self.mixture.p)
-            W_all = W_out
+            W_all = self.trainer.W_out
             if self.sharded:
-                W_all = dist.allgather_rows(W_out, [len(s) for s in self.shards])[self.inv]
+                W_all = dist.allgather_rows(W_all, [len(s) for s in self.shards])[self.inv]
             p = self.mixture.solve(W_all, None, self.lr_p, slot=t % 2)
             self.agg.run(W_all, p, self.W_g)
+            self.plan.round(t, self.lr, P[2])
+        elif self.sharded:
+            self.plan.round(t, self.lr, P[1])
+            dist.allreduce_sum_(self.W_g)
+            self.plan.round(t, self.lr, P[2])
         else:
-            self.agg.run(W_out, self.p_mine, self.W_g)
-            if self.sharded:
-                dist.allreduce_sum_(self.W_g)
-        self.evaluator.run(self.W_g, self.eval_hist[t])
+            self.plan.round(t, self.lr, P[1] | P[2])
         if self.W_hist is not None:
             self.W_hist[t].copy_(self.W_g)
         self.t += 1
+        if self.t < self.R:
+            self._prepare(self.t)
 
     def results(self):
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""
