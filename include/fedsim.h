@@ -116,7 +116,8 @@ int fs_eval(const float* d_phi, int64_t ld, const int32_t* d_labels, int n, cons
             double* d_out, double* d_ws, void* stream);
 
 /* ------------------------------------------------------------------------- *
- * FedAMW mixture step 1: Z[v][c*N + n] = sum_d X_val[v][d] * W_n[c][d]
+ * FedAMW mixture step 1: Z[v][c*ldN + n] = sum_d X_val[v][d] * W_n[c][d], where
+ * ldN = (N + 3) & ~3 (d_Z holds n_val * C * ldN floats; padding columns are 0)
  * (the inner matmul of tools.py:448, hoisted out of the p-SGD loop because the
  * stacked W of tools.py:435-440 is fixed during it).  fp32 MFMA GEMM.
  * ------------------------------------------------------------------------- */
@@ -126,7 +127,7 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
 /* ------------------------------------------------------------------------- *
  * FedAMW mixture step 2: `epochs` passes of SGD(momentum) on p over the pooled
  * validation set (tools.py:441-453): per batch of <= Bv rows (order from d_perms,
- * [epochs][n_val]): out[b,c] = sum_n p_n Z[v_b][c*N+n]; CE mean; grad_p;
+ * [epochs][n_val]): out[b,c] = sum_n p_n Z[v_b][c*ldN+n]; CE mean; grad_p;
  * buf = first ? grad : momentum*buf + grad; p -= lr_p*buf.  d_p, d_buf [N] are
  * updated in place; *d_first (int) is read and cleared (the momentum buffer of
  * torch.optim.SGD starts empty, tools.py:423).  One persistent workgroup.

@@ -60,15 +60,6 @@ struct SplitWS {
   int SZ;
 };
 
-// Workgroup barrier for LDS hand-offs only.  __syncthreads() carries a workgroup-scope
-// release that drains vmcnt -- i.e. waits for the next slice's loads in flight; this waits
-// for this wave's LDS operations (lgkmcnt) and nothing else.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 __device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
 
 // LDS image of one step's batch slice: row-major, row stride RS = DS + 8 floats, and the

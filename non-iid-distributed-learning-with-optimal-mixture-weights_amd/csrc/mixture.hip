@@ -1,6 +1,7 @@
 // FedAMW mixture-weight estimation (/root/reference/functions/tools.py:435-453).
 //
-// fs_mix_z:     Z[v][c*N + n] = X_val[v] . W_n[c]          -- fp32 MFMA GEMM, MFMA-bound
+// fs_mix_z:     Z[v][c*ldN + n] = X_val[v] . W_n[c]        -- fp32 MFMA GEMM, MFMA-bound
+//               (ldN = N rounded up to 4; the padding columns are written as zeros)
 //               (M = n_val, N = C*clients, K = D).  The reference recomputes this matmul
 //               for every 16-row batch of every inner epoch (tools.py:448); W is fixed
 //               during the p-solve, so it is computed once per round here.
@@ -8,8 +9,12 @@
 //               persistent workgroup (a grid-wide barrier per step would cost more than
 //               the step): out = Z_b p, CE, grad_p = Z_b^T g, momentum update.
 #include "common.h"
+#include "lanes.h"
 
 namespace fs {
+
+// client stride of a Z row segment: N rounded up to 4 (16-byte aligned class segments)
+__host__ __device__ __forceinline__ int mix_ldn(int N) { return (N + 3) & ~3; }
 
 // ----------------------------------------------------------------------------
 // Z GEMM: 64 x 64 output tile per 256-thread workgroup, BK = 16, LDS-staged,
@@ -22,7 +27,8 @@ __global__ __launch_bounds__(256) void mix_z_kernel(const float* __restrict__ W,
   __shared__ float As[MZ_BM][MZ_BK + MZ_PAD];
   __shared__ float Bs[MZ_BN][MZ_BK + MZ_PAD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
-  const int CN = C * N;
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;                          // padded columns: c * ldN + n, n < ldN
   const int v0 = blockIdx.y * MZ_BM;
   const int c0 = blockIdx.x * MZ_BN;
   // loader mapping: thread -> (row, 4-float group) of a 64 x 16 tile
@@ -32,8 +38,8 @@ __global__ __launch_bounds__(256) void mix_z_kernel(const float* __restrict__ W,
   const int cb = c0 + lr;
   const float* brow = nullptr;
   if (cb < CN) {
-    const int c = cb / N, n = cb - c * N;
-    brow = W + ((int64_t)n * C + c) * ld;
+    const int c = cb / ldN, n = cb - c * ldN;
+    if (n < N) brow = W + ((int64_t)n * C + c) * ld;   // padding clients: zero columns
   }
   const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
   floatx4 acc[2][2];
@@ -89,6 +95,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_kernel(const float* __re
                                                               float* __restrict__ p, float* __restrict__ buf,
                                                               int* __restrict__ first_flag) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ldN = mix_ldn(N);
   float* ps = smem;                       // [N]
   float* bs = ps + N;                     // [N]
   float* outs = bs + N;                   // [MS_MAXB][C]
@@ -96,7 +103,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_kernel(const float* __re
   int* vid = reinterpret_cast<int*>(gs + MS_MAXB * C);  // [MS_MAXB]
   int* vy = vid + MS_MAXB;                              // [MS_MAXB]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int CN = C * N;
+  const int CN = C * ldN;
   for (int n = tid; n < N; n += MS_THREADS) { ps[n] = p[n]; bs[n] = buf[n]; }
   int first = *first_flag;
   const int nbat = (nv + Bv - 1) / Bv;
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_kernel(const float* __re
       // out[b][c] = sum_n p_n Z[v_b][c*N + n]
       for (int q = w; q < bc * C; q += MS_WAVES) {
         const int b = q / C, c = q - b * C;
-        const float* zr = Z + (int64_t)vid[b] * CN + (int64_t)c * N;
+        const float* zr = Z + (int64_t)vid[b] * CN + (int64_t)c * ldN;
         float a = 0.f;
         for (int n = lane; n < N; n += 64) a += ps[n] * zr[n];
         a = wave_sum(a);
@@ -141,7 +148,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_kernel(const float* __re
         float gp = 0.f;
         for (int b = 0; b < bc; ++b) {
           const float* zr = Z + (int64_t)vid[b] * CN + n;
-          for (int c = 0; c < C; ++c) gp += gs[b * C + c] * zr[(int64_t)c * N];
+          for (int c = 0; c < C; ++c) gp += gs[b * C + c] * zr[(int64_t)c * ldN];
         }
         {
 #pragma clang fp contract(off)
@@ -181,8 +188,9 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_staged_kernel(const floa
                                                                      float* __restrict__ buf,
                                                                      int* __restrict__ first_flag) {
   extern __shared__ __attribute__((aligned(16))) float smem2[];
-  const int CN = C * N;
-  const int CN4 = (CN + 3) & ~3;                   // row stride in LDS (float4 aligned)
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int CN4 = CN;                              // row stride in LDS (ldN % 4 == 0: float4 aligned)
   float* zb = smem2;                               // [2][Bv][CN4]
   float* ps = zb + 2 * Bv * CN4;                   // [N]
   float* bs = ps + N;                              // [N]
@@ -253,7 +261,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_staged_kernel(const floa
 #pragma unroll
           for (int k = 0; k < MS2_NK; ++k) {
             const int n = lane + 64 * k;
-            if (n < N) a += ps[n] * zr[c * N + n];
+            if (n < N) a += ps[n] * zr[c * ldN + n];
           }
         }
         o[c] = wave_sum(a);                          // every lane holds out[b][c]
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_staged_kernel(const floa
 #pragma unroll
           for (int k = 0; k < MS2_NK; ++k) {
             const int n = lane + 64 * k;
-            if (n < N) gacc[k] += gv * zr[c * N + n];
+            if (n < N) gacc[k] += gv * zr[c * ldN + n];
           }
         }
       }
@@ -305,6 +313,237 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_staged_kernel(const floa
   if (tid == 0 && total > 0) *first_flag = 0;
 }
 
+// ----------------------------------------------------------------------------
+// p-solve, register-resident form (Bv <= 16, N <= 64*NK): the latency-optimised path.
+// Wave w owns batch row w of every step; lane l owns clients n = NK*l + j (j < NK) in EVERY
+// wave, so p and the momentum buffer live in registers (each wave updates its copy
+// redundantly, bitwise identically).  A step:
+//   logits    lane partials v[c] = sum_j Z[v_b][c][n_j] p[n_j], then a reduce-scatter over
+//             the 64 lanes on DPP / permlane swaps (lanes.h): lane l ends with the full
+//             out[b][l / (64/CP)]
+//   softmax   max / sum over the class groups (xor exchanges); the CE gradient of lane l's
+//             class, g = (softmax - onehot) / bc (torch's log_softmax backward)
+//   grad_p    g[c] broadcast by readlane; lane partial sum_c g[c] Z[v_b][c][n_j]; wave
+//             partials through LDS (double-buffered by step parity: ONE raw barrier per
+//             step), summed in wave order by every wave, then the momentum step
+//             (torch.optim.SGD, two roundings).
+// Z rows never touch LDS: each step's row segment is ONE dword / dwordx2 / dwordx4 load per
+// class per lane into a 3-deep register ring (the loads of step s+3 are issued as soon as
+// step s's data is consumed; CL + 2 loads per step keep 3 steps under the 63-deep vmcnt
+// window); the batch's row indices and labels are fetched one step earlier still.
+// ----------------------------------------------------------------------------
+// torch.optim.SGD(momentum) on one element: buf = first ? g : mom*buf + g; p -= lr*buf,
+// every product and sum rounded separately (no fma contraction)
+__device__ __forceinline__ void momentum_step(float& p, float& b, float g, int first, float mom, float lr) {
+#pragma clang fp contract(off)
+  const float nb = first ? g : mom * b + g;   // buf.mul_(0.9).add_(grad)
+  b = nb;
+  p = p + (-lr) * nb;                         // p.add_(buf, alpha=-lr)
+}
+
+constexpr int MR_WAVES = 16;
+
+// Diagnostic build only (-DFS_MIX_STAMPS, `make stamps`): per-phase cycle sums of wave 0,
+// written after the solver's buf[N] as buf[N + 8 + 2k] (uint64); never in the shipped library.
+#ifdef FS_MIX_STAMPS
+#define MR_STAMP(k)                                                                       \
+  {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (k > 0) mr_acc[k > 0 ? k - 1 : 0] += t_ - mr_prev;                                 \
+    mr_prev = t_;                                                                         \
+  }
+#else
+#define MR_STAMP(k)
+#endif
+
+template <int NK> struct MRVec;
+template <> struct MRVec<1> { typedef float T; };
+template <> struct MRVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
+template <> struct MRVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
+template <int NK>
+__device__ __forceinline__ float mr_el(const typename MRVec<NK>::T& v, int j) {
+  if constexpr (NK == 1) return v;
+  else return v[j];
+}
+
+template <int NK, int CP, int CL, int MR_DEPTH>
+__global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const float* __restrict__ Z,
+                                                                     const int32_t* __restrict__ y,
+                                                                     const int32_t* __restrict__ perms, int N,
+                                                                     int C, int nv, int epochs, int Bv, float lr,
+                                                                     float mom, float* __restrict__ p,
+                                                                     float* __restrict__ buf,
+                                                                     int* __restrict__ first_flag) {
+  static_assert(CL <= CP && CP <= 32 && (CP & (CP - 1)) == 0, "class padding");
+  static_assert(MR_DEPTH * (CL + 2) <= 63 && (MR_DEPTH == 2 || MR_DEPTH == 3), "ring vs the vmcnt window");
+  typedef typename MRVec<NK>::T vec;
+  constexpr int LPC = 64 / CP;                     // lanes per class after the reduce-scatter
+  __shared__ __attribute__((aligned(16))) float gpart[2][MR_WAVES][NK * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int n0 = NK * lane;                        // this lane's first client
+  float pr[NK], br[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    const int n = n0 + j;
+    pr[j] = n < N ? p[n] : 0.f;                    // p stays 0 on padding clients
+    br[j] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  const float invB = 1.0f / (float)Bv;            // 1/|batch| of every full batch
+  // lane byte offset inside a class segment; lanes past ldN re-read the last vector (p = 0)
+  const uint32_t nbyte = 4u * (uint32_t)min(n0, ldN - NK);
+  vec zr[MR_DEPTH][CL];
+  int lab[MR_DEPTH];
+  int idxr[MR_DEPTH];                              // slot R: row indices (lanes < Bv) of step s + DEPTH
+  // Every load below is unconditional (out-of-range lanes read a clamped, valid address and
+  // their values are masked where used): a predicated load would make the compiler wait for
+  // it at the join, which serialises the ring.
+  auto row_of = [&](int st) -> int {               // perms entry of lane `lane` in step st
+    const int ep = st / nbat, sb = st - ep * nbat;
+    const int b = sb * Bv + lane;
+    const int64_t at = (lane < Bv && b < nv && st < total) ? (int64_t)ep * nv + b : 0;
+    return perms[at];                              // always a valid row of Z
+  };
+  auto bsize = [&](int st) -> int { return min(Bv, nv - (st % nbat) * Bv); };
+  // issue the loads of one step (row indices in `idxv`, lanes < Bv) into ring slot R
+#define MR_ISSUE(R_, IDXV_)                                                                \
+  {                                                                                        \
+    const int vrow_ = __builtin_amdgcn_readlane((IDXV_), w);                               \
+    const char* zp_ = reinterpret_cast<const char*>(Z + (int64_t)vrow_ * CN);              \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                       \
+      /* uniform class base (c >= C: masked in the softmax) + 32-bit lane byte offset */  \
+      const char* zc_ = zp_ + 4 * (int64_t)(min(c, C - 1) * ldN);                          \
+      zr[R_][c] = *reinterpret_cast<const vec*>(                                           \
+          __builtin_assume_aligned(zc_ + nbyte, 4 * NK)); /* ldN % 4 == 0 */               \
+    }                                                                                      \
+    lab[R_] = y[(IDXV_)];                                                                  \
+  }
+  {
+    const int i0 = row_of(0), i1 = row_of(1), i2 = row_of(2);
+    idxr[0] = row_of(MR_DEPTH);
+    idxr[1] = row_of(MR_DEPTH + 1);
+    if constexpr (MR_DEPTH == 3) idxr[2] = row_of(MR_DEPTH + 2);
+    MR_ISSUE(0, i0);
+    MR_ISSUE(1, i1);
+    if constexpr (MR_DEPTH == 3) MR_ISSUE(2, i2);
+    // drain the prologue once, so the loop header inherits only the loop's own load order
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+  }
+  // one step on ring slot R_
+#define MR_STEP(R_)                                                                        \
+  {                                                                                        \
+    if (s >= total) break;                                                                 \
+    MR_STAMP(0)                                                                            \
+    /* indices of step s+DEPTH were loaded DEPTH steps ago; fetch those of s+2*DEPTH */   \
+    const int idx_cur = idxr[R_];                                                          \
+    idxr[R_] = row_of(s + 2 * MR_DEPTH);                                                   \
+    const int bc = bsize(s);                                                               \
+    float gme[NK];                                                                         \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                           \
+    MR_STAMP(1)                                                                            \
+    if (w < bc) {                                                                          \
+      float v[CP];                                                                         \
+      _Pragma("unroll") for (int c = 0; c < CP; ++c) {                                     \
+        float a = 0.f;                                                                     \
+        if (c < CL) {                                                                      \
+          _Pragma("unroll") for (int j = 0; j < NK; ++j) a += mr_el<NK>(zr[R_][c], j) * pr[j]; \
+        }                                                                                  \
+        v[c] = a;                                                                          \
+      }                                                                                    \
+      const float o = class_totals<CP>(v, lane);                                           \
+      const int cls = lane / LPC;                                                          \
+      const bool real = cls < C;                                                           \
+      const float m = class_max<LPC>(real ? o : -INFINITY, lane);                          \
+      const float e = class_sum<LPC>(real ? expf(o - m) : 0.f, lane);                      \
+      const float lse = logf(e);                                                           \
+      const float invb = bc == Bv ? invB : 1.0f / (float)bc;                               \
+      const int yy = __builtin_amdgcn_readlane(lab[R_], w);                                \
+      const float g = (cls == yy ? -invb : 0.f) + expf(o - m - lse) * invb;                \
+      _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                     \
+        if (c < C) {                                                                       \
+          const float gc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(            \
+              __builtin_bit_cast(int, g), c * LPC));                                       \
+          _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] += gc * mr_el<NK>(zr[R_][c], j); \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+    MR_STAMP(2)                                                                            \
+    const int par = s & 1;                                                                 \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[par][w][n0 + j] = gme[j];         \
+    MR_ISSUE(R_, idx_cur);                                                                 \
+    MR_STAMP(3)                                                                            \
+    lds_barrier();                 /* not __syncthreads: that would drain the ring */     \
+    MR_STAMP(4)                                                                            \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                       \
+      float gp = 0.f;                                                                      \
+      _Pragma("unroll") for (int i = 0; i < MR_WAVES; ++i) gp += gpart[par][i][n0 + j];    \
+      if (n0 + j < N) momentum_step(pr[j], br[j], gp, first, mom, lr);                     \
+    }                                                                                      \
+    first = 0;                                                                             \
+    MR_STAMP(5)                                                                            \
+    ++s;                                                                                   \
+  }
+#ifdef FS_MIX_STAMPS
+  unsigned long long mr_acc[5] = {0, 0, 0, 0, 0}, mr_prev = 0;
+#endif
+  int s = 0;
+  for (;;) {
+    MR_STEP(0)
+    MR_STEP(1)
+    if constexpr (MR_DEPTH == 3) MR_STEP(2)
+  }
+#undef MR_STEP
+#undef MR_ISSUE
+  if (w == 0) {
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int n = n0 + j;
+      if (n < N) {
+        p[n] = pr[j];
+        buf[n] = br[j];
+      }
+    }
+    if (lane == 0 && total > 0) *first_flag = 0;
+#ifdef FS_MIX_STAMPS
+    if (lane < 5) reinterpret_cast<unsigned long long*>(buf + N + 8)[lane] = mr_acc[lane];
+#endif
+  }
+}
+
+template <int NK, int CP, int CL>
+static void launch_mix_reg(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                           int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+  constexpr int depth = 3 * (CL + 2) <= 63 ? 3 : 2;   // CL + 2 loads per step stay in the vmcnt window
+  hipLaunchKernelGGL((mix_solve_reg_kernel<NK, CP, CL, depth>), dim3(1), dim3(MR_WAVES * 64), 0, st, Z, y, perms,
+                     N, C, nv, epochs, Bv, lr, mom, p, buf, first);
+}
+
+// register-resident solver for (N, C, Bv) if an instance covers it
+static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                          int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+  if (Bv > MR_WAVES) return false;
+  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : (N <= 256 ? 4 : 0));
+#define MR_CASE(NK_, CP_, CL_)                                                                  \
+  if (nk == NK_ && C <= CL_) {                                                                  \
+    launch_mix_reg<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first); \
+    return true;                                                                                \
+  }
+  // (the ring holds DEPTH * CL * NK floats per lane: larger shapes take the LDS-staged solver)
+  MR_CASE(1, 2, 2) MR_CASE(1, 4, 4) MR_CASE(1, 8, 8) MR_CASE(1, 16, 10) MR_CASE(1, 16, 16) MR_CASE(1, 32, 24)
+  MR_CASE(2, 2, 2) MR_CASE(2, 4, 4) MR_CASE(2, 8, 8) MR_CASE(2, 16, 10)
+  MR_CASE(4, 2, 2) MR_CASE(4, 4, 4)
+#undef MR_CASE
+  return false;
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -315,7 +554,7 @@ extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, 
   FS_REQUIRE(ld >= 64 && ld % 64 == 0, "ld must be a positive multiple of 64");
   FS_REQUIRE(d_W_all && d_X_val && d_Z, "null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int CN = C * N;
+  const int CN = C * mix_ldn(N);                  // padded columns (zeros for n >= N)
   dim3 grid((CN + MZ_BN - 1) / MZ_BN, (n_val + MZ_BM - 1) / MZ_BM);
   hipLaunchKernelGGL(mix_z_kernel, grid, dim3(256), 0, st, d_W_all, d_X_val, ld, N, C, n_val, d_Z);
   FS_LAUNCH_CHECK();
@@ -329,23 +568,22 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
   FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
   hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
+  if (mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
   {
     // LDS-staged solver: two batches of Z rows + p, buf and the wave partials must fit
-    const int CN4 = (C * N + 3) & ~3;
+    const int CN4 = C * mix_ldn(N);
     const size_t lds2 = sizeof(float) * (2 * (size_t)Bv * CN4 + 2 * (size_t)N + (size_t)MS_WAVES * N);
-    if (N <= 64 * MS2_NK && C <= 32 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
-      const void* kfn = C <= 16 ? reinterpret_cast<const void*>(&mix_solve_staged_kernel<16>)
-                                : reinterpret_cast<const void*>(&mix_solve_staged_kernel<32>);
+    if (N <= 64 * MS2_NK && C <= 16 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
+      const void* kfn = reinterpret_cast<const void*>(&mix_solve_staged_kernel<16>);
       if (lds2 > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
         if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
       }
-      if (C <= 16)
-        hipLaunchKernelGGL(mix_solve_staged_kernel<16>, dim3(1), dim3(MS_THREADS), lds2, st0, d_Z, d_labels, d_perms,
-                           N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
-      else
-        hipLaunchKernelGGL(mix_solve_staged_kernel<32>, dim3(1), dim3(MS_THREADS), lds2, st0, d_Z, d_labels, d_perms,
-                           N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
+      hipLaunchKernelGGL(mix_solve_staged_kernel<16>, dim3(1), dim3(MS_THREADS), lds2, st0, d_Z, d_labels, d_perms, N,
+                         C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
       FS_LAUNCH_CHECK();
       return FS_OK;
     }

@@ -7,7 +7,8 @@ HBM layout (one GPU; see DESIGN.md "Data layout"):
   perms    [E*rows]     int32 this round's shuffles, client j epoch e at E*row_off[j] + e*n_j
   W_out    [N, C, ld]   fp32  the clients x params buffer (each client's trained weights)
   W_g      [C, ld]      fp32  global model
-  Z        [n_val, C*N] fp32  FedAMW validation logits per client (row v, column c*N+n)
+  Z        [n_val, C*ldN] fp32 FedAMW validation logits per client (row v, column c*ldN+n,
+                             ldN = N rounded up to 4, padding columns 0)
 Everything stays resident across rounds.  Per round the host draws the shuffle
 seeds from torch's global CPU generator (one vectorised call) and uploads them
 (pinned, double-buffered, async on the compute stream); the permutations themselves
@@ -287,7 +288,8 @@ class Mixture:
         if self.nv < 1:
             raise ValueError('empty validation set')
         self.momentum = float(momentum)
-        self.Z = torch.empty(self.nv, self.C * self.N, dtype=torch.float32, device=device)
+        self.ldN = (self.N + 3) // 4 * 4
+        self.Z = torch.empty(self.nv, self.C * self.ldN, dtype=torch.float32, device=device)
         self.p = p0.to(device=device, dtype=torch.float32).clone()
         self.buf = torch.zeros(self.N, dtype=torch.float32, device=device)
         self.first = torch.ones(1, dtype=torch.int32, device=device)

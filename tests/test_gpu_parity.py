@@ -178,6 +178,39 @@ def test_eval_unit_golden(amd):
     assert abs(acc - float(d['acc'])) <= 100.0 / len(d['y']) + 1e-4
 
 
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (10, 2, 203, 16),       # config 1 shape: register solver, NK=1, CP=2
+    (100, 10, 517, 16),     # config 2 shape: NK=2, CP=16 (10 loaded classes)
+    (64, 7, 130, 16),       # N exactly one lane per client
+    (129, 3, 77, 8),        # NK=4, Bv < 16 (idle waves), ragged last batch
+    (37, 20, 90, 16),       # C > 16: CP=32, 2-deep ring
+    (23, 5, 211, 24),       # Bv > 16: LDS-staged solver
+    (19, 24, 70, 20),       # Bv > 16 and C > 16: global-memory solver
+    (300, 4, 60, 16),       # N > 256: global-memory solver
+])
+def test_mix_solve_variants(amd, N, C, nv, Bv):
+    """fs_mix_solve (every solver variant it selects) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    rs = np.random.RandomState(N + C + nv)
+    D = 64
+    Ws = (rs.normal(size=(N, C, D)) * 0.5).astype(np.float32)
+    Xv = (np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=nv).astype(np.int64)
+    p0 = rs.dirichlet(np.ones(N)).astype(np.float32)
+    dev = torch.device('cuda')
+    mix = amd.engine.Mixture(torch.from_numpy(Xv), torch.from_numpy(yv), D, C, N, Bv, torch.from_numpy(p0), dev)
+    Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+    Wd[:, :, :D] = torch.from_numpy(Ws)
+    pr, br = p0, None
+    for rnd in range(2):
+        torch.manual_seed(70 + rnd)
+        mix.solve(Wd, amd.rng.draw_pass_seeds(2), 0.5)
+        torch.cuda.synchronize()
+        torch.manual_seed(70 + rnd)
+        pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, 0.5, 2, batch_size=Bv)
+        assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
+        assert np.abs(mix.buf.cpu().numpy() - br).max() <= 1e-4 * np.abs(br).max()
+
+
 def test_mix_z_and_solve_vs_oracle(amd):
     rs = np.random.RandomState(3)
     N, C, D, nv = 23, 5, 192, 211
@@ -195,7 +228,9 @@ def test_mix_z_and_solve_vs_oracle(amd):
         mix.solve(Wd, seeds, 0.05)
         torch.cuda.synchronize()
         Zref = np.einsum('ncd,vd->vcn', Ws, Xv).reshape(nv, C * N)
-        assert np.abs(mix.Z.cpu().numpy() - Zref).max() <= 1e-5 * np.abs(Zref).max()
+        Zgot = mix.Z.view(nv, C, mix.ldN).cpu().numpy()
+        assert (Zgot[:, :, N:] == 0).all()                       # padding clients
+        assert np.abs(Zgot[:, :, :N].reshape(nv, C * N) - Zref).max() <= 1e-5 * np.abs(Zref).max()
         torch.manual_seed(40 + rnd)
         if rnd == 0:
             pr, br = O.mixture_solve(list(Ws), Xv, yv, p0, None, 0.05, 3)
