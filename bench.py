@@ -41,23 +41,42 @@ from fedamw_amd.functions import tools  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 
+# BASELINE.json configs that fit one GPU, per-GPU shapes; config 4 is config 2's
+# FedAvg shape at 1,250 clients x 64 rows per GPU (10,000 clients on 8 GPUs).
+PRESETS = {
+    2: dict(algo='fedavg', clients=100, rows=512, D=2048, C=10, test=10000, shape='a9a'),
+    3: dict(algo='fedprox', clients=1000, rows=465, D=4096, C=7, test=50000, shape='covtype'),
+    4: dict(algo='fedavg', clients=1250, rows=64, D=2048, C=10, test=10000, shape='a9a'),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--algo', default='fedavg', choices=['fedavg', 'fedprox', 'fedamw'])
-    ap.add_argument('--clients', type=int, default=100, help='clients per GPU')
-    ap.add_argument('--rows', type=int, default=512, help='training rows per client')
-    ap.add_argument('--D', type=int, default=2048)
-    ap.add_argument('--C', type=int, default=10)
-    ap.add_argument('--test', type=int, default=10000)
-    ap.add_argument('--shape', default='a9a', choices=['a9a', 'covtype'])
+    ap.add_argument('--config', type=int, default=2, choices=sorted(PRESETS),
+                    help='BASELINE.json config preset (per-GPU shape); the flags below override it')
+    ap.add_argument('--algo', choices=['fedavg', 'fedprox', 'fedamw'])
+    ap.add_argument('--clients', type=int, help='clients per GPU')
+    ap.add_argument('--rows', type=int, help='training rows per client')
+    ap.add_argument('--D', type=int)
+    ap.add_argument('--C', type=int)
+    ap.add_argument('--test', type=int)
+    ap.add_argument('--shape', choices=['a9a', 'covtype'])
+    ap.add_argument('--rounds', type=int, help="the algorithm's `round` argument (LR schedule; FedAMW's inner "
+                                                'p-SGD epochs per round); default 100 = the reference default')
     ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--host-shuffle', action='store_true', help='replay shuffles on host threads, not the GPU')
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    a.custom = any(getattr(a, k) != v for k, v in PRESETS[a.config].items() if k != 'algo')
+    if a.rounds is None:
+        a.rounds = 100
+    return a
 
 
 def cpu_baseline(d, args, budget):
@@ -92,8 +111,9 @@ def cpu_baseline(d, args, budget):
                       'of the numpy oracle, %.1f s' % (rounds, len(Xs), args.rows, args.D, args.C, len(yt), el)}
 
 
-def load_traffic(kernel='local_train'):
-    path = os.path.join(ROOT, 'profiles', 'traffic_%s.json' % kernel)
+def load_traffic(tag, kernel='local_train'):
+    """PMC HBM bytes per launch measured for exactly this workload (profiles/), else None."""
+    path = os.path.join(ROOT, 'profiles', 'traffic_%s_%s.json' % (kernel, tag))
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f)
@@ -127,7 +147,7 @@ def main():
     for k, j in enumerate(shards[rank]):
         Xs[j], ys[j] = d['X_train'][k], d['y_train'][k]
     lr, mu = 0.5, (5e-4 if args.algo == 'fedprox' else 0.0)
-    R = args.warmup + args.steps
+    R = max(args.rounds, args.warmup + args.steps)
     vl = None
     if args.algo == 'fedamw':
         vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(d['X_val'], d['y_val']), batch_size=16,
@@ -172,7 +192,8 @@ def main():
     n_rows = int(fed.feats.rows)
     alg_bytes = 4.0 * E * n_rows * args.D + 8.0 * E * n_rows + 8.0 * N_loc * args.C * args.D
     achieved = alg_bytes / (lt_ms * 1e-3) / 1e9
-    traffic = load_traffic()
+    tag = 'c%d%s' % (args.config, '' if args.algo == PRESETS[args.config]['algo'] else '_' + args.algo)
+    traffic = None if args.custom else load_traffic(tag)
     out = {
         'metric': 'client-rounds/sec (whole node)',
         'value': N_loc * ws * args.steps / el,
@@ -185,9 +206,11 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
-        'data': 'synthetic (a9a-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)',
-        'config': {'workload': 'config 2: %s, %d clients/GPU x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
-                               'parallel clients' % (args.algo, N_loc, args.rows, args.D, args.C, E, B, args.test),
+        'data': 'synthetic (%s-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)' % args.shape,
+        'config': {'workload': '%s: %s, %d clients/GPU x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
+                               'round=%d, parallel clients'
+                               % ('custom' if args.custom else 'config %d' % args.config, args.algo, N_loc, args.rows,
+                                  args.D, args.C, E, B, args.test, R),
                    'algo': args.algo, 'clients_total': N_loc * ws, 'rows_per_client': args.rows, 'D': args.D,
                    'C': args.C, 'epochs': E, 'batch': B, 'test_rows': args.test, 'parallelism': 'clients%d' % ws},
         'roofline': {'kernel': 'fs_local_train', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,

@@ -44,7 +44,7 @@ _orig_test_loop = T.test_loop
 def _recording_test_loop(X_test, y_test, type='classification', model=None, batch_size=32):
     _trace['W'].append(model.classifier.weight.detach().clone().numpy())
     caller = sys._getframe(1)
-    if 'p' in caller.f_locals and caller.f_code.co_name in ('FedAMW', '_fedamw_par'):
+    if 'p' in caller.f_locals and caller.f_code.co_name in ('FedAMW', '_fedamw_par', 'FedAMW_OneShot'):
         _trace['p'].append(caller.f_locals['p'].detach().clone().numpy())
     return _orig_test_loop(X_test, y_test, type, model, batch_size)
 
@@ -251,7 +251,84 @@ def run_units():
                         seed=31, D=40, C=3, after=torch.empty(3, dtype=torch.int64).random_().numpy())
 
 
+# Single-shot algorithms (tools.py:240-326), called positionally as exp.py:116-123 calls them
+# (epoch = local_epoch * Round there; small here).
+ONESHOT_CASES = [
+    ('central', 'centralized', dict(seed=21, sizes=[45, 32, 7], n_test=50, n_raw=12, D=64, C=3),
+     dict(lr=0.5, epoch=3, batch_size=32, prox=False, mu=0.0, reg=False, lam=0.0)),
+    ('central_reg', 'centralized', dict(seed=22, sizes=[40, 1, 33], n_test=41, n_raw=10, D=96, C=5),
+     dict(lr=0.3, epoch=2, batch_size=32, prox=True, mu=0.02, reg=True, lam=0.002)),
+    ('distrib', 'distributed', dict(seed=23, sizes=[45, 32, 7, 64], n_test=50, n_raw=12, D=64, C=4),
+     dict(lr=0.5, epoch=3, batch_size=32, prox=False, mu=0.0, reg=False, lam=0.0)),
+    ('distrib_prox', 'distributed', dict(seed=24, sizes=[33, 65, 1, 20], n_test=61, n_raw=10, D=128, C=7),
+     dict(lr=0.5, epoch=2, batch_size=32, prox=True, mu=0.05, reg=True, lam=0.001)),
+    ('oneshot', 'fedamw_oneshot', dict(seed=25, sizes=[50, 30, 41], n_test=40, n_raw=10, D=48, C=3, val_frac=0.2),
+     dict(lr=0.5, epoch=4, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=3, lr_p=0.05)),
+    ('oneshot_b', 'fedamw_oneshot', dict(seed=26, sizes=[50, 30, 41, 66, 12], n_test=70, n_raw=10, D=64, C=5,
+                                         val_frac=0.2),
+     dict(lr=0.5, epoch=3, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-3, R=5, lr_p=0.2)),
+]
+
+
+def run_oneshot_case(name, algo, dk, hp):
+    d = synth(**dk)
+    Xs, ys, Xt, yt = _split(d)
+    C, D = dk['C'], dk['D']
+    _trace['W'].clear()
+    _trace['p'].clear()
+    pos = ('classification', C, D, hp['lr'], hp['epoch'], hp['batch_size'], hp['prox'], hp['mu'],
+           hp['reg'], hp['lam'])
+    torch.manual_seed(TORCH_SEED)
+    with contextlib.redirect_stdout(io.StringIO()):
+        if algo == 'centralized':
+            tr, tl, ta = T.Centralized(Xs, ys, Xt, yt, *pos)
+        elif algo == 'distributed':
+            tr, tl, ta = T.Distributed(Xs, ys, Xt, yt, *pos)
+        else:
+            vl = torch.utils.data.DataLoader(
+                torch.utils.data.TensorDataset(torch.from_numpy(d['X_val']), torch.from_numpy(d['y_val'])),
+                batch_size=16, shuffle=True)
+            tr, tl, ta = T.FedAMW_OneShot(Xs, ys, Xt, yt, vl, *pos, hp['R'], hp['lr_p'])
+    rec = dict(d)
+    rec.update({k: np.asarray(v) for k, v in hp.items()})
+    f = lambda v: np.asarray(v.detach().numpy() if isinstance(v, torch.Tensor) else v, dtype=np.float64)
+    rec.update(algo=algo, C=C, D=D, torch_seed=TORCH_SEED, train_loss=f(tr), test_loss=f(tl), test_acc=f(ta),
+               W=np.stack(_trace['W']), rng_after=torch.empty(4, dtype=torch.int64).random_().numpy())
+    if _trace['p']:
+        rec['p'] = np.stack(_trace['p'])
+    np.savez_compressed(os.path.join(OUT, 'single_' + name + '.npz'), **rec)
+    print(name, 'acc', np.round(f(ta), 2), 'loss', np.round(f(tr), 4))
+
+
+def run_rff():
+    """RFF + feature_mapping (tools.py:15-31) as exp.py:63 calls them: X_train reshaped to
+    (1, n, d), X_test (n_t, d); outputs (1, n, D) and (n_t, D)."""
+    for name, n, nt, d, D, sig, dens in (('rff_a9a', 300, 97, 123, 256, 0.1, 14 / 123),
+                                         ('rff_cov', 129, 40, 54, 200, 1.0, 0.3)):
+        rs = np.random.RandomState(len(name) + n)
+        X = (rs.rand(n, d) < dens).astype(np.float32)
+        if name == 'rff_cov':
+            X[:, :10] = rs.rand(n, 10)
+        Xt = (rs.rand(nt, d) < dens).astype(np.float32)
+        torch.manual_seed(100)
+        Xf, Xtf = T.feature_mapping(torch.from_numpy(X).reshape(1, n, d), torch.from_numpy(Xt), sig, D, 'gaussian')
+        after = torch.empty(4, dtype=torch.int64).random_().numpy()
+        torch.manual_seed(100)
+        W, b = T.RFF(d, sig, D)
+        np.savez_compressed(os.path.join(OUT, name + '.npz'), X=X, X_test=Xt, sigma=np.float64(sig), D=D,
+                            seed=100, phi=Xf.numpy(), phi_test=Xtf.numpy(), W_rff=W.numpy(), b_rff=b.numpy(),
+                            rng_after=after)
+        print(name, Xf.shape, Xtf.shape)
+
+
 if __name__ == '__main__':
-    run_units()
-    for case in CASES:
-        run_case(*case)
+    which = sys.argv[1:] or ['rounds', 'single', 'rff']
+    if 'rounds' in which:
+        run_units()
+        for case in CASES:
+            run_case(*case)
+    if 'single' in which:
+        for case in ONESHOT_CASES:
+            run_oneshot_case(*case)
+    if 'rff' in which:
+        run_rff()
