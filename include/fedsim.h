@@ -34,7 +34,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 3
+#define FS_ABI_VERSION 4
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -135,6 +135,20 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
 int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                  int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
                  int* d_first, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Random Fourier feature map.  Replaces RFF's use in feature_mapping
+ * (tools.py:22-31: `1 / np.sqrt(D) * torch.cos(torch.matmul(X, W) + b)`, called at
+ * exp.py:63 for the training and the test set with one draw of W, b):
+ *   d_out[i][k] = scale * cos(sum_j d_X[i][j] * d_W[j][k] + d_b[k])   (k < D)
+ *   d_out[i][k] = 0                                                   (D <= k < ldo)
+ * d_X [n][ldx] raw features (d used), d_W [d][D] row-major, d_b [D]; scale = 1/sqrt(D).
+ * The draw of W and b stays on the host generator (tools.py:15-19).  fp32 MFMA GEMM
+ * with the +b / cos / scale epilogue fused; phi written once, in the engine's padded
+ * layout when ldo > D.
+ * ------------------------------------------------------------------------- */
+int fs_feature_map(const float* d_X, int64_t ldx, const float* d_W, const float* d_b, int n, int d, int D,
+                   float scale, float* d_out, int64_t ldo, void* stream);
 
 
 /* ------------------------------------------------------------------------- *

@@ -35,6 +35,8 @@ _SIGS = {
     'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p]),
+    'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                 C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_plan_desc_size': (C.c_int64, []),
     'fs_plan_create': (C.c_int, [C.c_void_p, C.c_void_p]),
     'fs_plan_destroy': (C.c_int, [C.c_void_p]),
@@ -43,7 +45,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
 

@@ -303,13 +303,14 @@ class Mixture:
                                      ep * self.nv, self.Z.device)
         self.shuffler.prepare(seeds, slot, stream)
 
-    def solve(self, W_all, seeds, lr_p, slot=None):
+    def solve(self, W_all, seeds, lr_p, slot=None, z=True):
         """W_all: [N, C, ld] every client's weights; seeds: sampler seeds of the round's
         validation passes (one per inner epoch), or None when ``prepare`` already enqueued
-        them into ``slot``."""
+        them into ``slot``.  ``z=False`` reuses Z from the previous call (W_all unchanged)."""
         L = _lib.lib()
-        _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
-                              _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')
+        if z:
+            _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
+                                  _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')
         if seeds is not None:
             slot = 0
             if len(seeds) == 0:
@@ -323,3 +324,24 @@ class Mixture:
                                   _lib.stream_ptr()), 'fs_mix_solve')
         self.shuffler.release(slot)
         return self.p
+
+
+def feature_map(X, W, b, D, out=None, ldo=None):
+    """fs_feature_map: ``scale * cos(X W + b)`` (tools.py:27, 29) on the current stream.
+    X [n, d] (any device; copied to the GPU as fp32 if needed), W [d, D], b [D] -> out [n, ldo]
+    (default ldo = D; columns D..ldo-1 are written as 0)."""
+    dev = torch.device('cuda', torch.cuda.current_device())
+    X = torch.as_tensor(X).to(device=dev, dtype=torch.float32).contiguous()
+    W = torch.as_tensor(W).to(device=dev, dtype=torch.float32).reshape(-1, int(D)).contiguous()
+    b = torch.as_tensor(b).to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    n, d = X.shape
+    if W.shape[0] != d or b.numel() != D:
+        raise ValueError('feature_map: X [n, %d] needs W [%d, %d] and b [%d]' % (d, d, D, D))
+    ldo = int(ldo or D)
+    if out is None:
+        out = torch.empty(n, ldo, device=dev, dtype=torch.float32)
+    assert out.is_contiguous() and out.shape[1] == ldo and out.shape[0] >= n
+    scale = float(np.float32(1.0 / np.sqrt(D)))      # the float64 scalar torch multiplies in fp32
+    _lib.check(_lib.lib().fs_feature_map(_lib.ptr(X), d, _lib.ptr(W), _lib.ptr(b), n, d, int(D), scale,
+                                         _lib.ptr(out), ldo, _lib.stream_ptr()), 'fs_feature_map')
+    return out

@@ -37,7 +37,8 @@ from .. import dist, engine, rng
 from .. import _lib
 from .._lib import FedsimError
 
-__all__ = ['FedAvg', 'FedProx', 'FedAMW', 'Federation', 'update_learning_rate', 'init_weights']
+__all__ = ['FedAvg', 'FedProx', 'FedAMW', 'Centralized', 'Distributed', 'FedAMW_OneShot', 'Federation', 'RFF',
+           'feature_mapping', 'update_learning_rate', 'init_weights']
 
 
 def update_learning_rate(epoch, target_lr, T):
@@ -252,3 +253,180 @@ def FedAMW(X_train, y_train, X_test, y_test, validloader, type='classification',
     on the pooled validation set, ``round`` inner epochs per round), aggregate with p."""
     return _run('fedamw', X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
                 batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=stats, verbose=verbose)
+
+
+# --------------------------------------------------------------------------- #
+# Random Fourier features (tools.py:15-31)
+# --------------------------------------------------------------------------- #
+def RFF(d, sigma, D):
+    """tools.py:15-19: W ~ N(0, sigma) [d, D], b ~ U(0, 2 pi) [1, D], drawn on torch's global
+    CPU generator exactly as the reference draws them (Uniform.sample((1, D)) -> (1, D, 1) ->
+    view), then placed on the GPU."""
+    m = torch.distributions.Uniform(torch.tensor([0.0]), torch.tensor([2 * torch.pi]))
+    W = torch.normal(0, sigma, size=(d, D))
+    b = m.sample((1, D)).view(-1, D)
+    dev = _device()
+    return W.to(dev), b.to(dev)
+
+
+def feature_mapping(X_train, X_test, k_par=10, D=200, type='gaussian'):
+    """tools.py:22-31: one RFF draw, then ``1/sqrt(D) * cos(X W + b)`` for every slice of
+    ``X_train`` ([P, n, d]; exp.py:63 passes P = 1) and for ``X_test`` -- each map one
+    fs_feature_map launch (MFMA GEMM with the cos epilogue fused).  Returns GPU tensors
+    [P, n, D] and [n_t, D]; other ``type`` values return the inputs unchanged."""
+    if type != 'gaussian':
+        return X_train, X_test
+    X_train = torch.as_tensor(X_train)
+    W, b = RFF(X_train[0].shape[1], k_par, D)
+    out = torch.empty(X_train.shape[0], X_train.shape[1], D, device=W.device, dtype=torch.float32)
+    for i in range(len(X_train)):
+        engine.feature_map(X_train[i], W, b, D, out=out[i])
+    return out, engine.feature_map(X_test, W, b, D)
+
+
+# --------------------------------------------------------------------------- #
+# Single-shot algorithms (tools.py:240-326)
+# --------------------------------------------------------------------------- #
+def _chain_train(X_train, y_train, W_init, D, C, lr, epoch, batch_size, prox, mu, reg, lam, dev):
+    """One shared model trained by the clients in turn (tools.py:263-266 / 284-287: train_loop
+    mutates the one ``model``), each for ``epoch`` epochs and anchored (prox) to its start --
+    one fs_local_train launch in chained mode.  Consumes the generator like the reference
+    (epoch passes per client, client-major).  Returns (feats, W_out [N, C, ld], loss [N])."""
+    feats = engine.Features([torch.as_tensor(x) for x in X_train], [torch.as_tensor(y) for y in y_train], D, dev)
+    trainer = engine.LocalTrainer(feats, C, batch_size, epoch, chained=True)
+    trainer.upload_perms(rng.draw_pass_seeds(trainer.N * epoch))
+    W0 = torch.zeros(C, feats.ld, device=dev, dtype=torch.float32)
+    W0[:, :D].copy_(W_init)
+    W_out, loss = trainer.run(W0, lr, prox, mu, reg, lam, chained=True)
+    return feats, trainer, W_out, loss
+
+
+def _test(evaluator, W, out2):
+    rng.draw_pass_seeds(1)                  # test_loop's shuffled pass (tools.py:219-220)
+    evaluator.run(W, out2)
+
+
+def _print_tests(ev, verbose):
+    if verbose and dist.world()[0] == 0:
+        for tl, ta in ev:
+            print('Test loss: {}, \t Test Acc: {}'.format(float(tl), float(ta)))
+
+
+def Centralized(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01,
+                epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=False, lambda_reg=0.01, *,
+                stats=None, verbose=True):
+    """tools.py:240-255: every client's rows concatenated (client order), ONE train_loop of
+    ``epoch`` epochs (exp.py:116 passes local_epoch * Round), one test_loop.  Returns
+    (train_loss, test_loss, test_acc) as Python floats, like the reference's Meter averages."""
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0)
+    dev = _device()
+    C = int(num_classes)
+    W_init = init_weights(D, C)
+    Xc = torch.cat([torch.as_tensor(x).to(dev, torch.float32) for x in X_train], 0)
+    yc = torch.cat([torch.as_tensor(y).reshape(-1).to('cpu', torch.int64) for y in y_train], 0)
+    feats, trainer, W_out, loss = _chain_train([Xc], [yc], W_init, D, C, lr, epoch, batch_size, prox, mu,
+                                               lambda_reg_if, lambda_reg, dev)
+    ev = engine.Evaluator(X_test, y_test, D, C, dev, feats.ld)
+    out2 = torch.empty(2, dtype=torch.float64, device=dev)
+    _test(ev, W_out[0], out2)
+    trainer.check_errors()
+    res = out2.cpu().numpy()
+    _print_tests([res], verbose)
+    if stats is not None:
+        stats.update(W_global=W_out[0, :, :D].detach().clone())
+    return float(loss[0].item()), float(res[0]), float(res[1])
+
+
+def Distributed(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01,
+                epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=False, lambda_reg=0.01, *,
+                stats=None, verbose=True):
+    """tools.py:258-276: chained local training of ``epoch`` epochs per client, one
+    n_j-weighted aggregate (fs_aggregate, the reference's left fold), one test_loop.  Returns
+    (train_loss 0-dim fp32 tensor, test_loss float, test_acc float)."""
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0)
+    dev = _device()
+    C = int(num_classes)
+    W_init = init_weights(D, C)
+    ns = np.array([len(y) for y in y_train])
+    p = torch.tensor(ns / sum(ns), dtype=torch.float32)
+    feats, trainer, W_out, loss = _chain_train(X_train, y_train, W_init, D, C, lr, epoch, batch_size, prox, mu,
+                                               lambda_reg_if, lambda_reg, dev)
+    ld = feats.ld
+    agg = engine.Aggregator(len(ns), C, ld, dev, chunks=1)
+    W_g = torch.empty(C, ld, device=dev, dtype=torch.float32)
+    agg.run(W_out, p.to(dev), W_g)
+    ev = engine.Evaluator(X_test, y_test, D, C, dev, ld)
+    out2 = torch.empty(2, dtype=torch.float64, device=dev)
+    _test(ev, W_g, out2)
+    trainer.check_errors()
+    res = out2.cpu().numpy()
+    train_loss = torch.sum(p * torch.tensor([float(v) for v in loss.cpu().numpy()]))    # tools.py:268
+    _print_tests([res], verbose)
+    if stats is not None:
+        stats.update(W_global=W_g[:, :D].detach().clone())
+    return train_loss, float(res[0]), float(res[1])
+
+
+def FedAMW_OneShot(X_train, y_train, X_test, y_test, validloader, type='classification', num_classes=10, D=200,
+                   lr=0.01, epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=True, lambda_reg=0.01,
+                   round=100, lr_p=5e-5, *, stats=None, verbose=True):
+    """tools.py:279-326: chained local training once (``epoch`` epochs per client), then
+    ``round`` times: one pass of plain SGD (no momentum, tools.py:300) on the mixture weights
+    over the validation loader, aggregate, test_loop.  Z = the stacked client models applied
+    to the validation set is computed once (fs_mix_z; the stack is fixed, tools.py:293-297).
+
+    The reference's aggregate compounds: ``global_weights = local_weights[0]``
+    aliases client 0's state dict, so from round 1 on the fold starts from the previous
+    global model: W(t) = W(t-1) * p0(t) + sum_{j>0} p_j(t) W_j (W(-1) = W_0).  Reproduced with
+    two fs_aggregate launches per round (a 1-client fold scales W(t-1) by p0(t) into row 0 of
+    a copy of the clients x params buffer; the N-client fold with weight 1 on that row adds
+    the rest), bitwise the reference's sequence of roundings.
+    Returns (train_loss 0-dim fp32 tensor, test_loss [round], test_acc [round])."""
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round)
+    dev = _device()
+    C, R = int(num_classes), int(round)
+    W_init = init_weights(D, C)
+    ns = np.array([len(y) for y in y_train])
+    N = len(ns)
+    p0 = torch.tensor(ns / np.sum(ns), dtype=torch.float32)
+    feats, trainer, W_out, loss = _chain_train(X_train, y_train, W_init, D, C, lr, epoch, batch_size, prox, mu,
+                                               lambda_reg_if, lambda_reg, dev)
+    ld = feats.ld
+    Xv, yv = validloader.dataset.tensors[:2]
+    if not isinstance(validloader.sampler, torch.utils.data.RandomSampler):
+        raise NotImplementedError('validloader must shuffle (exp.py:99)')
+    mix = engine.Mixture(Xv, yv, D, C, N, int(validloader.batch_size), p0, dev, ld, momentum=0.0)
+    ev = engine.Evaluator(X_test, y_test, D, C, dev, ld)
+    agg1 = engine.Aggregator(1, C, ld, dev, chunks=1)
+    aggN = engine.Aggregator(N, C, ld, dev, chunks=1)
+    W_agg = W_out.clone()                       # row 0 rewritten every round, rows 1.. = W_j
+    W_prev = W_out[0].clone()
+    q = torch.ones(N, dtype=torch.float32, device=dev)
+    W_g = torch.empty(C, ld, device=dev, dtype=torch.float32)
+    eval_hist = torch.empty(max(R, 1), 2, dtype=torch.float64, device=dev)
+    p_hist = torch.empty(max(R, 1), N, dtype=torch.float32, device=dev)
+    W_hist = torch.empty(R, C, ld, device=dev) if (stats is not None and stats.get('trace')) else None
+    for t in range(R):
+        seeds = rng.draw_pass_seeds(2)          # the validation pass, then test_loop's pass
+        mix.solve(W_out, seeds[:1], lr_p, z=(t == 0))
+        agg1.run(W_prev, mix.p, W_agg[0])       # W(t-1) * p0(t), in place in the reference
+        if N > 1:
+            q[1:].copy_(mix.p[1:])
+        aggN.run(W_agg, q, W_g)
+        W_prev.copy_(W_g)
+        p_hist[t].copy_(mix.p)
+        if W_hist is not None:
+            W_hist[t].copy_(W_g)
+        ev.run(W_g, eval_hist[t])
+    trainer.check_errors()
+    train_loss = torch.sum(p0 * torch.tensor([float(v) for v in loss.cpu().numpy()]))   # tools.py:292
+    evh = eval_hist[:R].cpu().numpy()
+    _print_tests(evh, verbose)
+    test_loss = torch.tensor(evh[:, 0], dtype=torch.float32) if R else torch.zeros(0)
+    test_acc = torch.tensor(evh[:, 1], dtype=torch.float32) if R else torch.zeros(0)
+    if stats is not None:
+        stats.update(W_global=W_g[:, :D].detach().clone(), p=mix.p.detach().clone())
+        if stats.get('trace'):
+            stats['p_rounds'] = p_hist[:R].cpu().numpy()
+            stats['W_rounds'] = W_hist[:, :, :D].cpu().numpy()
+    return train_loss, test_loss, test_acc

@@ -298,3 +298,108 @@ def FedAMW(X_train, y_train, X_test, y_test, X_val, y_val, type='classification'
         ptr.append(p.copy())
         tl[t], ta[t] = test_eval(Xt, yt, Wg, batch_size)
     return tr, tl, ta, {'W': np.stack(Wtr), 'p': np.stack(ptr)}
+
+
+# --------------------------------------------------------------------------- #
+# single-shot algorithms -- tools.py:240-326
+# --------------------------------------------------------------------------- #
+def _chain(Xs, ys, W, lr, epoch, batch_size, prox, mu, reg, lam):
+    """One shared ``model`` trained by every client in turn (tools.py:263-266, 284-287):
+    client i starts from client i-1's weights, anchored (prox) to that start."""
+    Ws, losses = [], []
+    for X, y in zip(Xs, ys):
+        W, l = train_client(X, y, W, lr, epoch, batch_size, prox, mu, reg, lam)
+        Ws.append(W)
+        losses.append(l)
+    return Ws, losses
+
+
+def Centralized(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01,
+                epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=False, lambda_reg=0.01):
+    """tools.py:240-255: all clients' rows concatenated in client order, one train_loop of
+    ``epoch`` epochs, one test_loop.  Returns (train_loss, test_loss, test_acc, trace)."""
+    Xs = _as_np_list(X_train, F32)
+    ys = _as_np_list(y_train, np.int64)
+    W = mlp_init(D, num_classes)
+    W, loss = train_client(np.concatenate(Xs), np.concatenate(ys), W, lr, epoch, batch_size, prox, mu,
+                           lambda_reg_if, lambda_reg)
+    tl, ta = test_eval(np.asarray(X_test, F32), np.asarray(y_test, np.int64), W, batch_size)
+    return loss, tl, ta, {'W': W[None]}
+
+
+def Distributed(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01,
+                epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=False, lambda_reg=0.01):
+    """tools.py:258-276: chained local training of ``epoch`` epochs per client, one
+    n_j-weighted aggregate (left fold), one test_loop."""
+    Xs = _as_np_list(X_train, F32)
+    ys = _as_np_list(y_train, np.int64)
+    W = mlp_init(D, num_classes)
+    p = _weights(ys)
+    Ws, losses = _chain(Xs, ys, W, lr, epoch, batch_size, prox, mu, lambda_reg_if, lambda_reg)
+    tr = np.sum(p * np.asarray(losses, dtype=F32), dtype=F32)                     # tools.py:268
+    Wg = aggregate(Ws, p)
+    tl, ta = test_eval(np.asarray(X_test, F32), np.asarray(y_test, np.int64), Wg, batch_size)
+    return tr, tl, ta, {'W': Wg[None]}
+
+
+def FedAMW_OneShot(X_train, y_train, X_test, y_test, X_val, y_val, type='classification', num_classes=10,
+                   D=200, lr=0.01, epoch=200, batch_size=32, prox=False, mu=0.1, lambda_reg_if=True,
+                   lambda_reg=0.01, round=100, lr_p=5e-5, val_batch_size=16):
+    """tools.py:279-326: chained local training once; then ``round`` times: one pass of plain
+    SGD (no momentum, tools.py:300) on p over the validation set, aggregate, test_loop.
+
+    The aggregate compounds: ``global_weights = local_weights[0]`` aliases client
+    0's state DICT (tools.py:317), ``*= p[0]`` scales its tensor in place and the fold rebinds the
+    dict entry to the sum (tools.py:318-321), so from round 1 on the fold starts from the
+    previous round's global model: W(t) = W(t-1) * p0(t) + sum_{j>0} p_j(t) W_j, with
+    W(-1) = W_0.  The p-solve reads the stack taken before the loop (tools.py:293-297)."""
+    Xs = _as_np_list(X_train, F32)
+    ys = _as_np_list(y_train, np.int64)
+    Xt = np.asarray(X_test, F32)
+    yt = np.asarray(y_test, np.int64)
+    W = mlp_init(D, num_classes)
+    p = _weights(ys)
+    Ws, losses = _chain(Xs, ys, W, lr, epoch, batch_size, prox, mu, lambda_reg_if, lambda_reg)
+    tr = np.sum(p * np.asarray(losses, dtype=F32), dtype=F32)                     # tools.py:292 (initial p)
+    S = Ws[0].copy()
+    tl = np.zeros(round, F32)
+    ta = np.zeros(round, F32)
+    Wtr, ptr = [], []
+    for t in range(round):
+        p, _ = mixture_solve(Ws, X_val, y_val, p, None, lr_p, 1, val_batch_size, momentum=0.0)
+        Wg = aggregate([(S * p[0]).astype(F32)] + Ws[1:], np.concatenate([[F32(1.0)], p[1:]]).astype(F32))
+        S = Wg
+        Wtr.append(Wg)
+        ptr.append(p.copy())
+        tl[t], ta[t] = test_eval(Xt, yt, Wg, batch_size)
+    return tr, tl, ta, {'W': np.stack(Wtr), 'p': np.stack(ptr)}
+
+
+# --------------------------------------------------------------------------- #
+# random Fourier features (SURVEY.md 8(a) A1) -- tools.py:15-31
+# --------------------------------------------------------------------------- #
+def rff(d, sigma, D):
+    """tools.py:15-19: W ~ N(0, sigma) (d x D) then b ~ U(0, 2pi) drawn as Uniform.sample((1, D))
+    -> shape (1, D, 1) -> view(-1, D); Uniform.rsample is low + rand * (high - low)."""
+    W = torch.normal(0, sigma, size=(d, D)).numpy()
+    r = torch.rand(1, D, 1).numpy().reshape(1, D)
+    b = (F32(0.0) + r * (F32(2 * torch.pi) - F32(0.0))).astype(F32)
+    return W.astype(F32), b
+
+
+def feature_map(X, W, b, D):
+    """tools.py:27, 29: 1/sqrt(D) * cos(X W + b), in float32 (the float64 scale is a
+    wrapped scalar: torch multiplies in the tensor's dtype)."""
+    z = (np.asarray(X, F32) @ W + b).astype(F32)
+    return (F32(1.0 / np.sqrt(D)) * np.cos(z)).astype(F32)
+
+
+def feature_mapping(X_train, X_test, k_par=10, D=200, type='gaussian'):
+    """tools.py:22-31: X_train is (P, n, d) (exp.py:63 passes P = 1); one RFF draw shared by
+    train and test.  Non-gaussian types return the inputs unchanged."""
+    if type != 'gaussian':
+        return X_train, X_test
+    X_train = np.asarray(X_train, F32)
+    W, b = rff(X_train[0].shape[1], k_par, D)
+    tr = np.stack([feature_map(x, W, b, D) for x in X_train])
+    return tr, feature_map(X_test, W, b, D)
