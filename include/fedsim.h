@@ -150,6 +150,20 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
 int fs_feature_map(const float* d_X, int64_t ldx, const float* d_W, const float* d_b, int n, int d, int D,
                    float scale, float* d_out, int64_t ldo, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * Data heterogeneity of a partition (exp.py:67-74):
+ *   fs_gram:   d_G[a][b] = sum_r phi[r][a] * phi[r][b] over rows [0, rows)   (D x D, row
+ *              stride ldg; exactly symmetric).  `torch.matmul(X.T, X)` of exp.py:67
+ *              before the division by len.
+ *   fs_hetero: d_S[j] = sum_{a,b} (G[a][b] / n_total - G_j[a][b] / n_j)^2 with G_j the
+ *              Gram of client j's rows [row_off[j], row_off[j+1]) (never materialised);
+ *              the caller forms sum_j n_j / n_total * sqrt(d_S[j]) (exp.py:73).
+ * phi [rows][ld] fp32 packed by client, ld % 64 == 0, columns >= D ignored.  MFMA SYRK.
+ * ------------------------------------------------------------------------- */
+int fs_gram(const float* d_phi, int64_t ld, int64_t rows, int D, float* d_G, int64_t ldg, void* stream);
+int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, int D, const float* d_G,
+              int64_t ldg, int64_t n_total, double* d_S, void* stream);
+
 
 /* ------------------------------------------------------------------------- *
  * Round plan: the native round driver.  One fs_plan_round call enqueues the

@@ -37,6 +37,9 @@ _SIGS = {
                                C.c_void_p]),
     'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                  C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),
+    'fs_gram': (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
+    'fs_hetero': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                            C.c_void_p, C.c_void_p]),
     'fs_plan_desc_size': (C.c_int64, []),
     'fs_plan_create': (C.c_int, [C.c_void_p, C.c_void_p]),
     'fs_plan_destroy': (C.c_int, [C.c_void_p]),

@@ -345,3 +345,24 @@ def feature_map(X, W, b, D, out=None, ldo=None):
     _lib.check(_lib.lib().fs_feature_map(_lib.ptr(X), d, _lib.ptr(W), _lib.ptr(b), n, d, int(D), scale,
                                          _lib.ptr(out), ldo, _lib.stream_ptr()), 'fs_feature_map')
     return out
+
+
+def heterogeneity(feats):
+    """exp.py:67-74 over a client-packed feature buffer (``Features``): fs_gram for
+    G = Phi^T Phi, fs_hetero for S_j = ||G/n - G_j/n_j||_F^2 per client.  Returns
+    (sum_j n_j/n * sqrt(S_j), S [N] numpy float64)."""
+    dev = feats.phi.device
+    D, N, n = feats.D, len(feats.ns), int(feats.rows)
+    if n < 1:
+        raise ValueError('heterogeneity of an empty partition')
+    G = torch.empty(D, D, device=dev, dtype=torch.float32)
+    S = torch.empty(N, device=dev, dtype=torch.float64)
+    L = _lib.lib()
+    _lib.check(L.fs_gram(_lib.ptr(feats.phi), feats.ld, n, D, _lib.ptr(G), D, _lib.stream_ptr()), 'fs_gram')
+    _lib.check(L.fs_hetero(_lib.ptr(feats.phi), feats.ld, _lib.ptr(feats.row_off_dev), N, D, _lib.ptr(G), D, n,
+                           _lib.ptr(S), _lib.stream_ptr()), 'fs_hetero')
+    S = S.cpu().numpy()
+    hete = np.float32(0.0)
+    for nj, s in zip(feats.ns, S):      # data_hete += len_j / len * torch.norm(C - C_j), an fp32 tensor
+        hete = np.float32(hete + np.float32(nj / n * np.float32(np.sqrt(s))))
+    return float(hete), S

@@ -403,3 +403,73 @@ def feature_mapping(X_train, X_test, k_par=10, D=200, type='gaussian'):
     W, b = rff(X_train[0].shape[1], k_par, D)
     tr = np.stack([feature_map(x, W, b, D) for x in X_train])
     return tr, feature_map(X_test, W, b, D)
+
+
+# --------------------------------------------------------------------------- #
+# exp.py's data preparation -- exp.py:60-99,
+# utils.py:314-349.  Restatements; the reference's utils.py cannot be imported here
+# (top-level torchvision import), so the partitioner is checked by properties and by
+# agreement with the product's host code, not against reference output.
+# --------------------------------------------------------------------------- #
+def dirichlet_partition(labels, n_clients, alpha):
+    """utils.py:314-349 (psizes = [1/n_clients] * n_clients, exp.py -> utils.py:125)."""
+    labels = np.asarray(labels)
+    K = len(set(labels.tolist()))
+    N = len(labels)
+    np.random.seed(2020)
+    min_size = 0
+    while min_size < 10:
+        idx_batch = [[] for _ in range(n_clients)]
+        for k in range(K):
+            idx_k = np.where(labels == k)[0]
+            np.random.shuffle(idx_k)
+            prop = np.random.dirichlet(np.repeat(alpha, n_clients))
+            prop = np.array([q * (len(b) < N / n_clients) for q, b in zip(prop, idx_batch)]) + 1 / len(idx_k)
+            prop = prop / prop.sum()
+            cut = (np.cumsum(prop) * len(idx_k)).astype(int)[:-1]
+            idx_batch = [b + piece.tolist() for b, piece in zip(idx_batch, np.split(idx_k, cut))]
+            min_size = min(len(b) for b in idx_batch)
+    for b in idx_batch:
+        np.random.shuffle(b)
+    return idx_batch
+
+
+def heterogeneity(phi_all, parts):
+    """exp.py:66-74: sum_j n_j/n * ||Phi^T Phi / n - Phi_j^T Phi_j / n_j||_F (float32 matrices,
+    float64 norms -- the checker's accumulation is more accurate than torch's)."""
+    phi_all = np.asarray(phi_all, F32)
+    n = len(phi_all)
+    C = (phi_all.T @ phi_all).astype(F32) / F32(n)
+    h = 0.0
+    for idx in parts:
+        X = phi_all[np.asarray(idx, dtype=np.int64)]
+        Cj = (X.T @ X).astype(F32) / F32(len(X))
+        h += len(X) / n * float(np.sqrt(np.sum(((C - Cj).astype(np.float64)) ** 2)))
+    return h
+
+
+def exp_prepare(X, y, Xt, yt, n_clients, alpha, k_par, D):
+    """exp.py:60-99 on raw arrays (the loaded LIBSVM data): partition (numpy reseeded to
+    2020), full-batch train pass (2 draws + randperm) and test pass (1 draw), RFF, per-client
+    20/80 validation split (np.random.shuffle).  Call after torch.manual_seed(100) /
+    np.random.seed(100).  Returns dict(parts, X_train, y_train, X_val, y_val, X_test, hete)."""
+    parts = dirichlet_partition(y, n_clients, alpha)
+    order = pass_order(len(y))                                          # exp.py:61
+    pass_order(len(yt), shuffle=False)                                  # exp.py:62
+    X, y = np.asarray(X, F32)[order], np.asarray(y)[order].astype(np.int64)
+    tr, te = feature_mapping(X[None], Xt, k_par, D)
+    phi = tr.reshape(-1, D)
+    Xc = [phi[np.asarray(i, dtype=np.int64)] for i in parts]
+    yc = [y[np.asarray(i, dtype=np.int64)] for i in parts]
+    hete = heterogeneity(phi, parts)
+    Xv, yv, Xs, ys = [], [], [], []
+    for Xi, yi in zip(Xc, yc):
+        r = np.arange(len(Xi))
+        np.random.shuffle(r)
+        cut = int(len(Xi) * 0.2)
+        Xv.append(Xi[r[:cut]])
+        yv.append(yi[r[:cut]])
+        Xs.append(Xi[r[cut:]])
+        ys.append(yi[r[cut:]])
+    return dict(parts=parts, X_train=Xs, y_train=ys, X_val=np.concatenate(Xv), y_val=np.concatenate(yv),
+                X_test=te, hete=hete)

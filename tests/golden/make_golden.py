@@ -322,7 +322,7 @@ def run_rff():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['rounds', 'single', 'rff']
+    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params']
     if 'rounds' in which:
         run_units()
         for case in CASES:
@@ -332,3 +332,11 @@ if __name__ == '__main__':
             run_oneshot_case(*case)
     if 'rff' in which:
         run_rff()
+    if 'params' in which:
+        # get_parameter (optimal_parameters.py) for every dataset it names + two that fall through
+        import json
+        import re
+        from functions.optimal_parameters import get_parameter
+        names = re.findall(r"dataset == '([^']+)'", open(os.path.join(REF, 'functions', 'optimal_parameters.py')).read())
+        with open(os.path.join(OUT, 'params.json'), 'w') as f:
+            json.dump({n: get_parameter(n) for n in names + ['a9a', 'covtype']}, f, indent=1)
