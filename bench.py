@@ -47,6 +47,9 @@ PRESETS = {
     2: dict(algo='fedavg', clients=100, rows=512, D=2048, C=10, test=10000, shape='a9a'),
     3: dict(algo='fedprox', clients=1000, rows=465, D=4096, C=7, test=50000, shape='covtype'),
     4: dict(algo='fedavg', clients=1250, rows=64, D=2048, C=10, test=10000, shape='a9a'),
+    # config 5 whole on one GPU: FedAMW (mixture-weight solve every round) over 1000 clients x
+    # (128 train + 32 validation rows), D = 16384 (the p-solve is replicated per GPU anyway)
+    5: dict(algo='fedamw', clients=1000, rows=128, D=16384, C=10, test=10000, shape='a9a'),
 }
 
 

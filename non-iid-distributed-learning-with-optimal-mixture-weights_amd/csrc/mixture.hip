@@ -11,6 +11,8 @@
 #include "common.h"
 #include "lanes.h"
 
+#include <cstdlib>
+
 namespace fs {
 
 // client stride of a Z row segment: N rounded up to 4 (16-byte aligned class segments)
@@ -544,6 +546,234 @@ static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, cons
   return false;
 }
 
+// ----------------------------------------------------------------------------
+// p-solve, multi-CU form (Bv <= 16, C <= 16, N <= 2048).  One workgroup on one CU cannot
+// stream a batch of Z rows faster than ~33 GB/s (gathered rows from the Infinity Cache,
+// MI355X_MICROARCH.md "Indexed rows"): at config 2 that is 64 KB per step, ~2 us -- the
+// whole cost of the register solver.  Here K workgroups split the CLIENTS: workgroup k owns
+// clients [k*S, k*S + S) and reads only that slice of every Z row, so each step moves
+// 16*C*S*4 bytes per CU.  The only cross-CU dependence of a step is the logits
+// out[b][c] = sum_n p_n Z[v_b][c][n]: every workgroup publishes its 16 x C partial logits
+// as 8-byte {tag, value} granules (relaxed agent-scope stores: the data is its own flag,
+// cdna_hip_programming.md Guideline 16, R2 form), reads all K partial vectors back and sums
+// them in workgroup order -- identical bits everywhere, so every workgroup computes the same
+// softmax gradient g[b][c] with no second exchange.  The gradient of its own clients,
+// grad_n = sum_{b,c} g[b][c] Z[v_b][c][n], then needs only its own registers (a wave
+// reduce-scatter + 4 wave partials through LDS), and the momentum step is local.
+//
+// Thread t = (row b = t / 16, class slot c = t % 16): 256 threads = 16 rows x 16 slots; slot
+// c >= C loads a clamped class and carries g = 0.  The next step's Z slice (S floats per
+// thread) is loaded at the top of the step, so it streams while the exchange waits.
+// Placement: 8*K workgroups are launched and those with blockIdx % 8 == 0 participate, which
+// under round-robin dispatch puts all K on one XCD (the exchange stays inside one L2); any
+// other placement changes only speed.  Parity slots (step & 1) of the exchange buffer are
+// zeroed before each launch; tags are step + 1.  Every spin is bounded: a timeout sets the
+// error word and poisons p with NaN (the kernel still drains).
+// ----------------------------------------------------------------------------
+constexpr int MC_THREADS = 256;
+constexpr int MC_XCDS = 8;
+constexpr int MC_KMAX = 32;
+constexpr int MC_SLOT = 256;                     // granules per workgroup per parity
+constexpr unsigned MC_SPIN_LIMIT = 1u << 20;
+
+template <int S>
+__global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* __restrict__ Z,
+                                                                 const int32_t* __restrict__ y,
+                                                                 const int32_t* __restrict__ perms, int N, int C,
+                                                                 int nv, int epochs, int Bv, float lr, float mom,
+                                                                 float* __restrict__ p, float* __restrict__ buf,
+                                                                 int* __restrict__ first_flag,
+                                                                 unsigned long long* __restrict__ xbuf,
+                                                                 unsigned* __restrict__ err, int K) {
+  static_assert(S == 8 || S == 16 || S == 32 || S == 64, "slice width");
+  if (blockIdx.x % MC_XCDS) return;
+  constexpr int LPV = 64 / S;                      // lanes per value after the reduce-scatter
+  __shared__ __attribute__((aligned(16))) float ps[S];
+  __shared__ float gp[MC_THREADS / 64][S];
+  const int k = blockIdx.x / MC_XCDS;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = t >> 4, c = t & 15;
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int n_lo = k * S;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int myn = n_lo + t;                        // client of thread t < S
+  float pr = 0.f, br = 0.f;
+  if (t < S && myn < N) {
+    pr = p[myn];
+    br = buf[myn];
+  }
+  if (t < S) ps[t] = pr;                           // p = 0 on padding clients
+  int first = *first_flag;
+  // this thread's column offsets inside a row: class min(c, C-1), float4 i of the slice
+  // (past ldN: clamped to a valid vector, multiplied by p = 0 and its gradient discarded)
+  const int cc = min(c, C - 1);
+  int coff[S / 4];
+#pragma unroll
+  for (int i = 0; i < S / 4; ++i) coff[i] = cc * ldN + min(n_lo + 4 * i, ldN - 4);
+  auto row_at = [&](int st) -> int {              // Z row of (step st, row b), clamped
+    st = min(st, total - 1);
+    const int ep = st / nbat, sb = st - ep * nbat;
+    const int bc = min(Bv, nv - sb * Bv);
+    return perms[(int64_t)ep * nv + sb * Bv + (b < bc ? b : 0)];
+  };
+  float4 zc[S / 4];
+  int yc, vnext;
+  {
+    const int v0 = row_at(0);
+    const float* zr = Z + (int64_t)v0 * CN;
+#pragma unroll
+    for (int i = 0; i < S / 4; ++i) zc[i] = ld4(zr + coff[i]);
+    yc = y[v0];
+    vnext = row_at(1);
+  }
+  bool dead = false;
+  lds_barrier();
+  for (int st = 0; st < total; ++st) {
+    // ---- next step's slice streams behind this step ----
+    float4 zn[S / 4];
+    {
+      const float* zr = Z + (int64_t)vnext * CN;
+#pragma unroll
+      for (int i = 0; i < S / 4; ++i) zn[i] = ld4(zr + coff[i]);
+    }
+    const int yn = y[vnext];
+    const int vn2 = row_at(st + 2);
+    // ---- partial logits of this workgroup's clients ----
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < S / 4; ++i) {
+      const float4 pv = *reinterpret_cast<const float4*>(&ps[4 * i]);
+      a += zc[i].x * pv.x;
+      a += zc[i].y * pv.y;
+      a += zc[i].z * pv.z;
+      a += zc[i].w * pv.w;
+    }
+    // ---- exchange: publish, then gather all K partials (workgroup order) ----
+    const unsigned tag = (unsigned)st + 1u;
+    unsigned long long* slot = xbuf + (int64_t)(st & 1) * K * MC_SLOT;
+    const bool real = c < C;
+    float o = 0.f;
+    if (real) {
+      __hip_atomic_store(slot + (int64_t)k * MC_SLOT + t,
+                         ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(a), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long gr[MC_KMAX];
+      unsigned spins = 0;
+      for (;;) {
+#pragma unroll
+        for (int q = 0; q < MC_KMAX; ++q)
+          if (q < K) gr[q] = __hip_atomic_load(slot + (int64_t)q * MC_SLOT + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < MC_KMAX; ++q)
+          if (q < K) ok = ok && (unsigned)(gr[q] >> 32) == tag;
+        if (ok || dead) break;
+        if (++spins > MC_SPIN_LIMIT) {
+          dead = true;
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < MC_KMAX; ++q)
+        if (q < K) o += __uint_as_float((unsigned)gr[q]);
+    }
+    // ---- softmax-CE gradient of row b (16-lane class groups) ----
+    const int sb = st % nbat;
+    const int bc = min(Bv, nv - sb * Bv);
+    float m = real ? o : -INFINITY;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) m = fmaxf(m, xor_get(m, off, lane));
+    float e = real ? expf(o - m) : 0.f;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) e += xor_get(e, off, lane);
+    const float lse = logf(e);
+    const float invb = 1.0f / (float)bc;
+    const float g = (real && b < bc) ? (c == yc ? -invb : 0.f) + expf(o - m - lse) * invb : 0.f;
+    // ---- gradient of this workgroup's clients ----
+    float v[S];
+#pragma unroll
+    for (int i = 0; i < S / 4; ++i) {
+      v[4 * i + 0] = g * zc[i].x;
+      v[4 * i + 1] = g * zc[i].y;
+      v[4 * i + 2] = g * zc[i].z;
+      v[4 * i + 3] = g * zc[i].w;
+    }
+    const float tot = class_totals<S>(v, lane);    // lane l: wave sum of v[l / LPV]
+    if ((lane & (LPV - 1)) == 0) gp[w][lane / LPV] = tot;
+    lds_barrier();
+    if (t < S) {
+      const float gs = ((gp[0][t] + gp[1][t]) + gp[2][t]) + gp[3][t];
+      if (myn < N) momentum_step(pr, br, gs, first, mom, lr);
+      ps[t] = pr;
+    }
+    first = 0;
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < S / 4; ++i) zc[i] = zn[i];
+    yc = yn;
+    vnext = vn2;
+  }
+  if (t < S && myn < N) {
+    p[myn] = dead ? __int_as_float(0x7fc00000) : pr;
+    buf[myn] = br;
+  }
+  if (k == 0 && t == 0 && total > 0) *first_flag = 0;
+}
+
+// per-device exchange workspace of the multi-CU solver: [2][MC_KMAX][MC_SLOT] granules + error word
+static unsigned long long* g_mc_ws[64];
+
+static int mc_workspace(unsigned long long** out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(FS_EHIP, "fs_mix_solve: no device");
+  if (!g_mc_ws[dev]) {
+    void* q = nullptr;
+    const size_t bytes = sizeof(unsigned long long) * (2 * MC_KMAX * MC_SLOT + 8);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
+    if (hipMemset(q, 0, bytes) != hipSuccess) return fail(FS_EHIP, "fs_mix_solve: workspace memset");
+    g_mc_ws[dev] = reinterpret_cast<unsigned long long*>(q);
+  }
+  *out = g_mc_ws[dev];
+  return FS_OK;
+}
+
+// slice width for N clients (0: not covered): S clients per workgroup, K = ceil(ldN / S) <= 32
+static int mc_slice(int N) {
+  const int ldN = mix_ldn(N);
+  const char* env = getenv("FS_MIX_MC_S");
+  if (env) {
+    const int s = atoi(env);
+    if ((s == 8 || s == 16 || s == 32 || s == 64) && (ldN + s - 1) / s <= MC_KMAX) return s;
+  }
+  for (int s : {8, 16, 32, 64})
+    if ((ldN + s - 1) / s <= MC_KMAX && (s > 8 || ldN <= 128)) return s;
+  return 0;
+}
+
+static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
+                        int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+  const int S = mc_slice(N);
+  if (S == 0 || C > 16 || Bv > 16) return 1;     // not covered
+  const int K = (mix_ldn(N) + S - 1) / S;
+  unsigned long long* ws = nullptr;
+  if (int rc = mc_workspace(&ws)) return rc;
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned long long) * 2 * K * MC_SLOT, st);
+  if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
+  unsigned* err = reinterpret_cast<unsigned*>(ws + 2 * MC_KMAX * MC_SLOT);
+  const dim3 grid(MC_XCDS * K), block(MC_THREADS);
+#define MC_CASE(S_)                                                                                        \
+  if (S == S_)                                                                                             \
+    hipLaunchKernelGGL(mix_solve_mc_kernel<S_>, grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, \
+                       buf, first, ws, err, K);
+  MC_CASE(8) MC_CASE(16) MC_CASE(32) MC_CASE(64)
+#undef MC_CASE
+  return 0;
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -568,15 +798,31 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
   FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
   hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
-  if (mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
+  // solver choice: FS_MIX_SOLVER=auto (default) | mc | reg | staged | global (diagnostics
+  // and tests; a forced solver that does not cover the shape falls through to the next one)
+  const char* pick = getenv("FS_MIX_SOLVER");
+  const std::string want = pick ? pick : "auto";
+  // auto: the single-CU register solver where an instance covers the shape (no cross-CU
+  // exchange: ~1-2.5 us per step), else the multi-CU solver (~4-7 us per step, 7-11x the
+  // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
+  if ((want == "auto" || want == "reg") &&
+      mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
     FS_LAUNCH_CHECK();
     return FS_OK;
+  }
+  if (want == "auto" || want == "mc") {
+    const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
+    if (rc < 0) return rc;
+    if (rc == 0) {
+      FS_LAUNCH_CHECK();
+      return FS_OK;
+    }
   }
   {
     // LDS-staged solver: two batches of Z rows + p, buf and the wave partials must fit
     const int CN4 = C * mix_ldn(N);
     const size_t lds2 = sizeof(float) * (2 * (size_t)Bv * CN4 + 2 * (size_t)N + (size_t)MS_WAVES * N);
-    if (N <= 64 * MS2_NK && C <= 16 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
+    if (want != "global" && N <= 64 * MS2_NK && C <= 16 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
       const void* kfn = reinterpret_cast<const void*>(&mix_solve_staged_kernel<16>);
       if (lds2 > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);

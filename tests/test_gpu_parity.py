@@ -186,9 +186,9 @@ def test_eval_unit_golden(amd):
     (37, 20, 90, 16),       # C > 16: CP=32, 2-deep ring
     (23, 5, 211, 24),       # Bv > 16: LDS-staged solver
     (19, 24, 70, 20),       # Bv > 16 and C > 16: global-memory solver
-    (300, 4, 60, 16),       # N > 256: global-memory solver
+    (300, 4, 60, 16),       # N > 256: multi-CU solver
 ])
-def test_mix_solve_variants(amd, N, C, nv, Bv):
+def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
     """fs_mix_solve (every solver variant it selects) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
     rs = np.random.RandomState(N + C + nv)
     D = 64
@@ -203,12 +203,40 @@ def test_mix_solve_variants(amd, N, C, nv, Bv):
     pr, br = p0, None
     for rnd in range(2):
         torch.manual_seed(70 + rnd)
-        mix.solve(Wd, amd.rng.draw_pass_seeds(2), 0.5)
+        mix.solve(Wd, amd.rng.draw_pass_seeds(2), lr)
         torch.cuda.synchronize()
         torch.manual_seed(70 + rnd)
-        pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, 0.5, 2, batch_size=Bv)
+        pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, lr, 2, batch_size=Bv)
         assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
         assert np.abs(mix.buf.cpu().numpy() - br).max() <= 1e-4 * np.abs(br).max()
+
+
+@pytest.mark.parametrize('N,C,nv,Bv,S', [
+    (100, 10, 517, 16, None),   # config 2 shape: S = 8, K = 13 workgroups
+    (100, 10, 517, 16, 32),     # same, 4 workgroups of 32 clients
+    (1000, 10, 97, 16, None),   # config 5 client count: S = 32, K = 32
+    (300, 4, 60, 16, None),     # S = 16, ragged last slice
+    (129, 3, 77, 8, None),      # Bv < 16: idle rows, ragged last batch
+    (48, 16, 99, 16, 8),        # C = 16: every class slot real
+    (2000, 2, 45, 16, None),    # S = 64, K = 32
+    (5, 2, 40, 16, 8),          # one workgroup (K = 1)
+])
+def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
+    """fs_mix_solve's multi-CU solver (clients split over K workgroups, one partial-logit
+    exchange per step) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'mc')
+    if S:
+        monkeypatch.setenv('FS_MIX_MC_S', str(S))
+    # (at N >= 1000, lr_p = 0.5 drives p to |p| ~ 10 within a few steps, where any two fp32
+    # summation orders of the 10^4-term logits drift past 1e-5; the configs use lr_p ~ 1e-3)
+    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)
+
+
+@pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10)])
+def test_mix_solve_forced_fallbacks(amd, monkeypatch, solver, N, C):
+    """The single-workgroup solvers the auto choice no longer takes at these shapes."""
+    monkeypatch.setenv('FS_MIX_SOLVER', solver)
+    test_mix_solve_variants(amd, N, C, 133, 16)
 
 
 def test_mix_z_and_solve_vs_oracle(amd):
