@@ -14,7 +14,9 @@
  *     (hipMalloc / torch caching allocator); h_* are host pointers.
  *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All
  *     device entry points are asynchronous on that stream, allocate nothing and
- *     never synchronise (safe under hipGraph capture).
+ *     never synchronise (safe under hipGraph capture) -- except the first
+ *     multi-CU fs_mix_solve on a device, which allocates its 128 KB exchange
+ *     workspace once (call it once before capturing).
  *   - Feature rows are fp32, row-major, with a leading dimension `ld` that is a
  *     multiple of 64 floats (D is zero-padded to ld; padded columns stay exactly 0).
  *   - Return value: 0 on success, negative on error; fs_last_error() returns a
@@ -130,11 +132,21 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * [epochs][n_val]): out[b,c] = sum_n p_n Z[v_b][c*ldN+n]; CE mean; grad_p;
  * buf = first ? grad : momentum*buf + grad; p -= lr_p*buf.  d_p, d_buf [N] are
  * updated in place; *d_first (int) is read and cleared (the momentum buffer of
- * torch.optim.SGD starts empty, tools.py:423).  One persistent workgroup.
+ * torch.optim.SGD starts empty, tools.py:423).  A single persistent workgroup
+ * where a register-resident instance covers (N, C, Bv); otherwise (Bv <= 16,
+ * C <= 16, N <= 2048) K <= 32 workgroups that split the clients and exchange
+ * partial logits once per step; otherwise one LDS-staged / global workgroup.
+ * Calls on one device are serialised by the caller (the multi-CU solver keeps a
+ * per-device exchange workspace).  FS_MIX_SOLVER=reg|mc|staged|global forces one.
  * ------------------------------------------------------------------------- */
 int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                  int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
                  int* d_first, void* stream);
+
+/* Diagnostic (synchronous): 0 = no multi-CU solve has run on this device yet;
+ * 1 = one has (agent-scope exchange), +4 if any of its bounded spins timed out
+ * (the solve then wrote NaN into d_p). */
+int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *
  * Random Fourier feature map.  Replaces RFF's use in feature_mapping

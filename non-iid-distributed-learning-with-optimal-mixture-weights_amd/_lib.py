@@ -35,6 +35,7 @@ _SIGS = {
     'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p]),
+    'fs_mix_solve_last_mode': (C.c_int, []),
     'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                  C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_gram': (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),

@@ -778,6 +778,15 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
 
 using namespace fs;
 
+extern "C" int fs_mix_solve_last_mode(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_mc_ws[dev]) return 0;
+  unsigned err = 0;
+  if (hipMemcpy(&err, g_mc_ws[dev] + 2 * MC_KMAX * MC_SLOT, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 1 | (err ? 4 : 0);
+}
+
 extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val, float* d_Z,
                         void* stream) {
   FS_REQUIRE(N >= 1 && C >= 1 && n_val >= 1, "bad sizes");

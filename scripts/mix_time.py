@@ -46,6 +46,8 @@ zms, sms = ts[-1]
 print('N=%d C=%d n_val=%d epochs=%d: mix_z %.1f us (%.1f TFLOP/s), mix_solve %.2f ms = %.3f us/step over %d steps; '
       'p finite: %s' % (N, C, nv, ep, zms * 1e3, 2.0 * N * C * D * nv / zms / 1e9, sms, sms * 1e3 / steps, steps,
                         bool(torch.isfinite(mix.p).all())), flush=True)
+print('  solver %s, multi-CU state %d (0 = not run, 1 = ran, +4 = spin timeout)'
+      % (os.environ.get('FS_MIX_SOLVER', 'auto'), L.lib().fs_mix_solve_last_mode()), flush=True)
 if STAMPS:
     acc = mix.buf[N + 8:N + 18].cpu().numpy().view(np.uint64)
     names = ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update']

@@ -230,6 +230,8 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
     # (at N >= 1000, lr_p = 0.5 drives p to |p| ~ 10 within a few steps, where any two fp32
     # summation orders of the 10^4-term logits drift past 1e-5; the configs use lr_p ~ 1e-3)
     test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)
+    mode = amd.lib.lib().fs_mix_solve_last_mode()
+    assert mode == 1, mode             # the multi-CU solver ran, no spin timed out
 
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10)])
