@@ -220,6 +220,7 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
     (48, 16, 99, 16, 8),        # C = 16: every class slot real
     (2000, 2, 45, 16, None),    # S = 64, K = 32
     (5, 2, 40, 16, 8),          # one workgroup (K = 1)
+    (1100, 16, 40, 16, None),   # S = 64, C = 16
 ])
 def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
     """fs_mix_solve's multi-CU solver (clients split over K workgroups, one partial-logit
@@ -234,11 +235,12 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
     assert mode == 1, mode             # the multi-CU solver ran, no spin timed out
 
 
-@pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10)])
+@pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
+                                        ('mc', 1000, 7)])
 def test_mix_solve_forced_fallbacks(amd, monkeypatch, solver, N, C):
-    """The single-workgroup solvers the auto choice no longer takes at these shapes."""
+    """The solvers the auto choice does not take at these shapes."""
     monkeypatch.setenv('FS_MIX_SOLVER', solver)
-    test_mix_solve_variants(amd, N, C, 133, 16)
+    test_mix_solve_variants(amd, N, C, 133, 16, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
 
 
 def test_mix_z_and_solve_vs_oracle(amd):
