@@ -342,3 +342,39 @@ def test_device_randperm_matches_host_and_torch(amd, n):
     g = torch.Generator()
     g.manual_seed(int(seeds[-1]))
     np.testing.assert_array_equal(host[-n:], torch.randperm(n, generator=g).numpy())
+
+
+@pytest.mark.parametrize('N', [300, 1000])
+def test_fedamw_dropin_many_clients_vs_oracle(amd, N):
+    """The FedAMW drop-in end to end with more clients than any single-workgroup p-solver
+    covers (the multi-CU solver runs inside the round), parallel clients, vs the oracle."""
+    rs = np.random.RandomState(N)
+    D, C, R = 64, 4, 2
+    sizes = list(rs.randint(5, 30, size=N))
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    Xt = (np.cos(rs.normal(size=(90, D))) / np.sqrt(D)).astype(np.float32)
+    yt = rs.randint(0, C, size=90).astype(np.int64)
+    Xv = (np.cos(rs.normal(size=(150, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=150).astype(np.int64)
+    # lr_p small enough that p stays O(1): with |p| >> 1 the aggregate sum_j p_j W_j of 1000
+    # clients cancels, and any two fp32 p's within 1e-5 give W's further apart than 1e-5 max|W|
+    lr_p = 0.05 if N <= 300 else 0.005
+    T = torch.from_numpy
+    stats = {'trace': True}
+    torch.manual_seed(5)
+    tr, tl, ta = amd.tools.FedAMW([T(x) for x in Xs], [T(y) for y in ys], T(Xt), T(yt), _dl(Xv, yv),
+                                  'classification', C, D, 0.5, 2, 32, False, 0.0, True, 1e-3, R, lr_p,
+                                  clients='parallel', stats=stats, verbose=False)
+    assert amd.lib.lib().fs_mix_solve_last_mode() == 1     # the multi-CU solver ran, no spin timed out
+    torch.manual_seed(5)
+    otr, otl, ota, trace = O.FedAMW(Xs, ys, Xt, yt, Xv, yv, 'classification', C, D, 0.5, 2, 32, False, 0.0, True,
+                                    1e-3, R, lr_p, clients='parallel')
+    print('max|p| %.3g, max|W| %.3g' % (np.abs(trace['p']).max(), np.abs(trace['W']).max()))
+    W = stats['W_rounds']
+    for t in range(R):
+        assert np.abs(W[t] - trace['W'][t]).max() <= W_RTOL * np.abs(trace['W'][t]).max(), t
+    p = stats['p'].cpu().numpy()
+    assert np.abs(p - trace['p'][-1]).max() <= P_RTOL * np.abs(trace['p'][-1]).max()
+    np.testing.assert_allclose(tr.numpy(), otr, rtol=0, atol=LOSS_RTOL * max(1, np.abs(otr).max()))
+    np.testing.assert_allclose(tl.numpy(), otl, rtol=0, atol=LOSS_RTOL * max(1, np.abs(otl).max()))
+    assert np.abs(ta.numpy() - ota).max() <= 100.0 / 90 + 1e-4
