@@ -14,9 +14,13 @@
  *     (hipMalloc / torch caching allocator); h_* are host pointers.
  *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  All
  *     device entry points are asynchronous on that stream, allocate nothing and
- *     never synchronise (safe under hipGraph capture) -- except the first
- *     multi-CU fs_mix_solve on a device, which allocates its 128 KB exchange
- *     workspace once (call it once before capturing).
+ *     never synchronise (safe under hipGraph capture).  Kernels that exchange data
+ *     between workgroups take a caller-owned workspace: the launch zeroes its
+ *     exchange part itself; its LAST 256 bytes are an error block whose first
+ *     uint32 is set (sticky) when a bounded cross-workgroup wait timed out -- the
+ *     caller zeroes the workspace once at allocation, reads that word after the
+ *     work and clears it.  Test knob: FS_SPIN_LIMIT=0 in the environment makes
+ *     every such launch report a timeout (the error path without a real hang).
  *   - Feature rows are fp32, row-major, with a leading dimension `ld` that is a
  *     multiple of 64 floats (D is zero-padded to ld; padded columns stay exactly 0).
  *   - Return value: 0 on success, negative on error; fs_last_error() returns a
@@ -36,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 4
+#define FS_ABI_VERSION 5
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -82,10 +86,13 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              from d_W_start (parallel clients).
  *   G, d_ws    workgroups per client and their workspace, from fs_local_train_plan:
  *              G = 1: one workgroup walks each client (any shape, chained or not);
- *              G = 2/4: "split clients" -- G co-resident workgroups share one client's
- *              feature tiles and exchange partial logits every step (parallel mode,
- *              C <= 16, B <= 32, N*G <= CUs).  d_ws[0..3] is an error word: nonzero
- *              after the kernel means the plan was violated (results invalid).
+ *              G = 2/4/8/16: "split clients" -- a group of G co-resident workgroups
+ *              shares one client's feature tiles and exchanges partial logits every
+ *              step (C <= 16, B <= 32).  Parallel clients: min(N, CUs/G) groups walk
+ *              the clients (LPT order, snake over the groups); chained clients: one
+ *              group walks the chain with the weights kept in registers.  The error
+ *              word (last 256 bytes of d_ws) is nonzero after the kernel if a partner
+ *              never arrived (results invalid).
  * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
  * ------------------------------------------------------------------------- */
 int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int* G_out,
@@ -136,16 +143,18 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * where a register-resident instance covers (N, C, Bv); otherwise (Bv <= 16,
  * C <= 16, N <= 2048) K <= 32 workgroups that split the clients and exchange
  * partial logits once per step; otherwise one LDS-staged / global workgroup.
- * Calls on one device are serialised by the caller (the multi-CU solver keeps a
- * per-device exchange workspace).  FS_MIX_SOLVER=reg|mc|staged|global forces one.
+ * d_ws: fs_mix_solve_ws_bytes(N, C, Bv) bytes, zeroed once at allocation (the multi-CU
+ * exchange granules + the error block; a timed-out exchange also writes NaN into d_p).
+ * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=reg|mc|staged|global
+ * forces one solver.
  * ------------------------------------------------------------------------- */
+int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv);
 int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                  int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
-                 int* d_first, void* stream);
+                 int* d_first, void* d_ws, int64_t ws_bytes, void* stream);
 
-/* Diagnostic (synchronous): 0 = no multi-CU solve has run on this device yet;
- * 1 = one has (agent-scope exchange), +4 if any of its bounded spins timed out
- * (the solve then wrote NaN into d_p). */
+/* Diagnostic (host state only): the solver the calling thread's last fs_mix_solve
+ * launched -- 1 register-resident, 2 multi-CU, 3 LDS-staged, 4 global; 0 = none yet. */
 int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *

@@ -32,9 +32,10 @@ _SIGS = {
                           C.c_void_p, C.c_void_p]),
     'fs_mix_z': (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
                            C.c_void_p]),
+    'fs_mix_solve_ws_bytes': (C.c_int64, [C.c_int, C.c_int, C.c_int]),
     'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
-                               C.c_void_p]),
+                               C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_mix_solve_last_mode': (C.c_int, []),
     'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                  C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),
@@ -49,9 +50,11 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
+ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
+SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global'}
 
 
 class PlanDesc(C.Structure):

@@ -407,8 +407,10 @@ extern "C" int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_r
              prox ? 1 : 0, reg ? 1 : 0, chained ? 1 : 0, d_W_start, d_W_out, d_loss};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (G > 1) {
-    FS_REQUIRE(!chained, "split clients (G > 1) need parallel clients");
-    return launch_local_train_split(P, G, d_ws, ws_bytes, st);
+    const int rc = launch_local_train_split(P, G, d_ws, ws_bytes, st);
+    if (rc != FS_OK) return rc;
+    FS_LAUNCH_CHECK();
+    return FS_OK;
   }
   const int grid = chained ? 1 : N;
   const int RT = B <= 16 ? 1 : (B <= 32 ? 2 : 4);

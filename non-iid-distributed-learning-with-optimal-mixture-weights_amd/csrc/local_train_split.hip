@@ -1,39 +1,45 @@
-// Split-client local training: G workgroups (on G CUs) cooperate on ONE client.
+// Split-client local training: a GROUP of G workgroups (on G CUs) trains one client at a
+// time, each workgroup owning a slice of the feature dimension.
 //
-// Same math as local_train.hip (train_loop, /root/reference/functions/tools.py:177-215),
-// used when a round has fewer clients than the chip has CUs (e.g. BASELINE config 2:
-// 100 clients on 256 CUs, G = 2).  Workgroup g of a client owns a contiguous range of
-// 64-column feature tiles (its "slice"); wave w owns tiles w, w + 8, ...:
+// Same math as local_train.hip (train_loop, /root/reference/functions/tools.py:177-215).
+// Workgroup g of a group owns a contiguous range of 64-column feature tiles (its "slice");
+// wave w owns tiles w, w + 8:
 //   * its slice of the client's weights lives in REGISTERS for the whole local training
 //     (lane (c, k-slot) holds W[c][64T + 16 q + 4 k + e]), the prox anchor likewise;
 //   * each step's gathered batch rows of the slice arrive in REGISTERS in the forward's
 //     operand layout (64 contiguous bytes of 16 rows per load), so the forward
 //     z_g = X_b,g W_g^T (v_mfma_f32_16x16x4_f32) reads no LDS; the same registers are then
 //     written once into a bank-conflict-free LDS image that the backward
-//     grad_g^T = X_b,g^T G reads, and are refilled with the next step's rows (half of the
-//     waves issue those loads right after the hand-off, half after the softmax, so one wave
-//     of each SIMD computes while its partner is held up issuing loads);
-//   * per step the G partial logit tiles (plus the partial squared norms of W - W_a and W
-//     the prox / ridge terms need) are exchanged through a small global buffer as 8-byte
+//     grad_g^T = X_b,g^T G reads, and are refilled with the NEXT step's rows -- which may
+//     belong to the next client of the group's sequence, so the stream never drains at a
+//     client boundary;
+//   * per step the G partial logits (the B x C real ones only) plus the partial squared
+//     norms of W - W_a and W are exchanged through a small global buffer as 8-byte
 //     {tag, value} granules -- the write-through (sc1) store / sc1 load hand-off of
-//     cdna_hip_programming.md Guideline 16, R2 form (no fences, no flags) -- spread over
-//     all 8 waves; every workgroup sums the G partials in the same fixed order, so all of
-//     them compute bitwise-identical softmax gradients.
-// Co-residency: the G partners spin on each other, so the launcher uses this path only
-// when N*G workgroups fit on the device at one per CU; every spin is bounded and a
-// timeout is reported through the workspace error word instead of hanging the GPU.
-#include <atomic>
-
+//     cdna_hip_programming.md Guideline 16, R2 form (no fences, no flags); every workgroup
+//     sums the G partials in the same fixed order, so all of them compute bitwise-identical
+//     softmax gradients.
+// Work assignment:
+//   parallel clients  ngroups = min(N, CUs / G) groups walk the (LPT-ordered) clients in a
+//                     snake order, every client starting from W_start -- so any N runs
+//                     split, as persistent groups, not just N * G <= CUs;
+//   chained clients   ONE group walks clients 0..N-1 in order (reference semantics,
+//                     SURVEY Q1): the weights stay in the registers from one client to the
+//                     next and only the prox anchor is re-taken, so the strictly sequential
+//                     chain runs on G CUs instead of one.
+// Co-residency: the G partners spin on each other, so the grid never exceeds the CU count;
+// every spin is bounded and a timeout is reported through the workspace error word.
+// Hand-off tags are the group's step counter + 1 (32 bits): the exchange buffer is zeroed by
+// the launcher before every launch.
 #include "common.h"
 
 namespace fs {
 
 constexpr int SP_WAVES = 8;
 constexpr int SP_THREADS = SP_WAVES * 64;
+constexpr int SP_TPW = 2;                 // max 64-column tiles per wave (register budget)
 constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
-#ifndef SP_STAGGER_CYCLES
-#define SP_STAGGER_CYCLES 0
-#endif
+constexpr int SP_ERR_BYTES = 256;         // error block at the END of the workspace (never memset)
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -44,7 +50,7 @@ constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
     unsigned long long t_;                                                                \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
     __builtin_amdgcn_sched_barrier(0);                                                    \
-    if (k > 0) stamp_acc[k > 0 ? k - 1 : 0] += t_ - stamp_prev;                                     \
+    if (k > 0) stamp_acc[k > 0 ? k - 1 : 0] += t_ - stamp_prev;                           \
     stamp_prev = t_;                                                                      \
   }
 #else
@@ -53,11 +59,11 @@ constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
 
 struct SplitWS {
   unsigned* err;                       // [1] sticky; nonzero: a partner never arrived (spin bound hit)
-  unsigned long long* xbuf;            // [N][2][G][SZ] published partials: {tag, value} granules
+  unsigned long long* xbuf;            // [ngroups][2][G][SZ] published partials: {tag, value} granules
   unsigned long long* stamps;          // [grid][16] diagnostic build only
-  unsigned gen;                        // launch generation (1..65535): high half of every tag
-  int G;
-  int SZ;
+  int SZ;                              // granules per (group, parity, slice)
+  int ngroups;
+  unsigned spin_limit;                 // 0: test knob -- report a timeout at the first hand-off
 };
 
 __device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
@@ -70,15 +76,55 @@ __device__ __forceinline__ int img_off(int row, int RS, int tile, int blk) {
   return row * RS + 64 * tile + 4 * (blk ^ (row & 7));
 }
 
+// Client k of a group's sequence (-1: none).  Parallel: tier k of the LPT-ordered clients,
+// snake order (even tiers forward, odd tiers backward) so the groups' step totals balance.
+__device__ __forceinline__ int sp_client(const LTParams& P, int grp, int ng, int k) {
+  if (P.chained) return k < P.N ? k : -1;
+  const int idx = k * ng + ((k & 1) ? ng - 1 - grp : grp);
+  if (idx >= P.N) return -1;
+  return P.order ? P.order[idx] : idx;
+}
+
+// A position in the group's step sequence: client (k, j), step st of its E * nbat steps.
+struct SpCur {
+  int k, j, n, nbat, steps, st;
+  int64_t row0;
+};
+
+// first client with at least one step at sequence position >= k (false: sequence exhausted)
+__device__ __forceinline__ bool sp_seek(SpCur& c, const LTParams& P, int grp, int ng, int T, int k) {
+  for (; k < T; ++k) {
+    const int j = sp_client(P, grp, ng, k);
+    if (j < 0) continue;
+    const int64_t r0 = P.row_off[j];
+    const int n = (int)(P.row_off[j + 1] - r0);
+    const int nbat = (n + P.B - 1) / P.B;
+    if (nbat == 0 || P.E == 0) continue;
+    c.k = k; c.j = j; c.n = n; c.nbat = nbat; c.steps = P.E * nbat; c.st = 0; c.row0 = r0;
+    return true;
+  }
+  c.k = T;
+  return false;
+}
+
+__device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp, int ng, int T) {
+  if (c.k >= T) return false;
+  if (++c.st < c.steps) return true;
+  return sp_seek(c, P, grp, ng, T, c.k + 1);
+}
+
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
 // (fixed q) then reads 64 contiguous bytes of each of 16 rows.
-template <int RT, int G, int TPW, bool PROX>
+template <int RT, int G, bool PROX>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   constexpr int NW = SP_WAVES;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
+  constexpr int TPW = SP_TPW;
+  // exchanged values per thread: NR*C logits + 2 norms (G >= 8 requires NR*C + 2 <= 512)
+  constexpr int M = (G >= 8) ? 1 : (NZ + 2 + SP_THREADS - 1) / SP_THREADS;
   __shared__ float zpart[NW][NR][NC];
   __shared__ float gbuf[NR][NC];
   __shared__ float zsum[NR][NC];
@@ -88,75 +134,96 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   __shared__ float nrm[2];
   extern __shared__ __attribute__((aligned(16))) float xs_lds[];   // [NR][RS] batch slice image
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform for the compiler
   const int64_t ld = P.ld;
   const int NT = (int)(ld >> 6);
   const int C = P.C, B = P.B, E = P.E;
+  const int NV = NR * C + 2;
 
-  // block -> (client slot, slice): consecutive linear ids on one XCD under round-robin
-  // placement, so a client's partners mostly share an L2 (speed only, results unaffected)
+  // block -> (group, slice).  Chained: 8*G blocks are launched and those with
+  // blockIdx % 8 == 0 take part (one XCD under round-robin placement).  Parallel: consecutive
+  // linear ids on one XCD, so a group's partners mostly share an L2.  Speed only.
   const int nb = gridDim.x;
-  int lin = blockIdx.x;
-  if (nb % 8 == 0) lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
-  const int cs = lin / G, g = lin % G;
-  const int j = P.order ? P.order[cs] : cs;
+  int lin;
+  if (P.chained) {
+    if (blockIdx.x % 8) return;
+    lin = blockIdx.x / 8;
+  } else {
+    lin = blockIdx.x;
+    if (nb % 8 == 0) lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
+  }
+  const int ng = X.ngroups;
+  const int grp = lin / G, g = lin % G;
+  if (grp >= ng) return;
+  const int T = P.chained ? P.N : (P.N + ng - 1) / ng;     // client sequence length
   const int t0 = tile_lo(g, G, NT), t1 = tile_lo(g + 1, G, NT);
   const int NTS = t1 - t0;                       // tiles of this slice
   const int RS = NTS * 64 + 8;                   // LDS row stride (floats)
-  const int64_t row0 = P.row_off[j];
-  const int n = (int)(P.row_off[j + 1] - row0);
-  const int nbat = (n + B - 1) / B;
-  const int steps = E * nbat;
   const float* start = P.W_start;
-  float* Wj = P.W_out + (int64_t)j * C * ld;
-  unsigned long long* xb = X.xbuf + (int64_t)cs * 2 * G * X.SZ;
-  const int32_t* perm = P.perms + (int64_t)E * row0;
+  unsigned long long* xb = X.xbuf + (int64_t)grp * 2 * G * X.SZ;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // ---- weights (and prox anchor) of this slice into registers ----
+  // ---- weights (and prox anchor) of this slice into registers: the round-start model ----
   float4 wr[TPW][4], ar[TPW][4];
-  float nw0 = 0.f;
+  // (the weight addresses are rebuilt behind an empty asm at every use: they are used only at
+  // client boundaries and must not be hoisted into registers that live across the step loop)
+  auto wbase = [&]() {
+    int64_t b = (int64_t)l16 * ld + 64 * t0 + 4 * lg;
+    asm volatile("" : "+v"(b));
+    return b;
+  };
+  auto load_start = [&]() {
+    const int64_t base = wbase();
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int Tl = w + NW * i;
-    const bool ok = Tl < NTS && l16 < C;
+    for (int i = 0; i < TPW; ++i) {
+      const int Tl = w + NW * i;
+      const bool ok = Tl < NTS && l16 < C;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t off = (int64_t)l16 * ld + 64 * (t0 + Tl) + 16 * q + 4 * lg;
-      wr[i][q] = ok ? ld4(start + off) : zero4;
-      if (PROX) ar[i][q] = wr[i][q];
-      nw0 += wr[i][q].x * wr[i][q].x + wr[i][q].y * wr[i][q].y + wr[i][q].z * wr[i][q].z + wr[i][q].w * wr[i][q].w;
+      for (int q = 0; q < 4; ++q) {
+        wr[i][q] = ok ? ld4(start + base + 64 * Tl + 16 * q) : zero4;
+        s += wr[i][q].x * wr[i][q].x + wr[i][q].y * wr[i][q].y + wr[i][q].z * wr[i][q].z + wr[i][q].w * wr[i][q].w;
+      }
     }
-  }
-  if (steps == 0) {
+    return wave_sum(s);
+  };
+  auto store_w = [&](float* Wj) {
+    const int64_t base = wbase();
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int Tl = w + NW * i;
       if (Tl < NTS && l16 < C)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st4(Wj + (int64_t)l16 * ld + 64 * (t0 + Tl) + 16 * q + 4 * lg, wr[i][q]);
+        for (int q = 0; q < 4; ++q) st4(Wj + base + 64 * Tl + 16 * q, wr[i][q]);
     }
-    if (g == 0 && tid == 0) P.loss[j] = 0.0;
-    return;
-  }
-  nw0 = wave_sum(nw0);
+  };
+  const float nw0 = load_start();                // ||W_start||^2 partial of this wave
   if (lane == 0) { wred[w][0] = 0.f; wred[w][1] = nw0; }
 
   // ---- the batch slice lives in registers in the forward's operand layout: lane (l16, lg)
   // holds rows rt*16 + l16, columns 16 q + 4 lg .. +3 of each of its tiles.  Rows past the
   // batch end load a valid row (their logits are ignored, their softmax gradient is 0).
-  // The shuffle entry of a step's rows is fetched one step before its features.
-  auto pos_of = [&](int st_, int r_) {
-    const int e_ = st_ / nbat, s_ = st_ - e_ * nbat;
-    const int b0_ = s_ * B, bc_ = min(B, n - b0_);
-    return e_ * n + b0_ + (r_ < bc_ ? r_ : 0);
-  };
+  // `lc` is the step whose rows pn[] address (global row indices, fetched one step before
+  // the features); it runs one step ahead of the compute loop, across client boundaries.
   float4 xf[TPW][RT][4];
   int pn[RT], lb[RT];
+  SpCur lc;
+  bool lc_ok = sp_seek(lc, P, grp, ng, T, 0);
+  auto fetch_rows = [&]() {
+    const int e_ = lc.st / lc.nbat, s_ = lc.st - e_ * lc.nbat;
+    const int b0_ = s_ * B, bc_ = min(B, lc.n - b0_);
+    const int32_t* pp_ = P.perms + (int64_t)E * lc.row0 + (int64_t)e_ * lc.n + b0_;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r_ = rt * 16 + l16;
+      pn[rt] = (int)(lc.row0 + pp_[r_ < bc_ ? r_ : 0]);
+    }
+  };
 #define SP_XLOAD()                                                                   \
   {                                                                                  \
     _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {                              \
-      const int64_t r_ = row0 + pn[rt];                                              \
+      const int64_t r_ = pn[rt];                                                     \
       if (w == 0 && lg == 0) lb[rt] = P.labels[r_];                                  \
       const float* src_ = P.phi + r_ * ld + 64 * t0 + 4 * lg;                        \
       _Pragma("unroll") for (int i = 0; i < TPW; ++i)                                \
@@ -165,51 +232,102 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
             xf[i][rt][q] = ld4(src_ + 64 * (w + NW * i) + 16 * q);                   \
     }                                                                                \
   }
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) pn[rt] = perm[pos_of(0, rt * 16 + l16)];
-  SP_XLOAD();
-  if (steps > 1)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) pn[rt] = perm[pos_of(1, rt * 16 + l16)];
+  if (lc_ok) {
+    fetch_rows();
+    SP_XLOAD();
+    lc_ok = sp_advance(lc, P, grp, ng, T);
+    if (lc_ok) fetch_rows();
+  }
   __syncthreads();
 
+  // clients with no step (n_j = 0 or E = 0): the result is the client's start -- the
+  // current weights in a chain, W_start for parallel clients; their loss is 0
+  auto flush_empty = [&](int ka, int kb) {
+    for (int k = ka; k < kb; ++k) {
+      const int j = sp_client(P, grp, ng, k);
+      if (j < 0) continue;
+      float* Wj = P.W_out + (int64_t)j * C * ld;
+      if (P.chained) {
+        store_w(Wj);
+      } else {
+        const int64_t base = wbase();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          const int Tl = w + NW * i;
+          if (Tl < NTS && l16 < C)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int64_t off = base + 64 * Tl + 16 * q;
+              st4(Wj + off, ld4(start + off));
+            }
+        }
+      }
+      if (g == 0 && tid == 0) P.loss[j] = 0.0;
+    }
+  };
+
+  // the compute loop walks the group's steps with its own cursor `cc` (one flat loop: the
+  // client boundaries are branches inside it)
+  SpCur cc;
+  bool cc_ok = sp_seek(cc, P, grp, ng, T, 0);
+  flush_empty(0, cc_ok ? cc.k : T);
+  unsigned gs = 0;                                // steps run by this group in this launch
+  bool dead = false;                              // a hand-off timed out: stop waiting
   double lsum = 0.0;
 #ifdef FS_STAMPS
   unsigned long long stamp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
 #endif
-  for (int st = 0; st < steps; ++st) {
-    SP_STAMP(0)
-    const int e = st / nbat, s = st - e * nbat;
-    const int b0 = s * B, bc = min(B, n - b0);
-    const int par = st & 1;
-    const unsigned tag32 = (X.gen << 16) | (unsigned)(st + 1);
-    const bool more = st + 1 < steps;
-    if (w == 0 && lg == 0)
+  for (; cc_ok; ++gs) {
+    const int st = cc.st, n = cc.n, nbat = cc.nbat;
+    if (st == 0) {
+      // client start: parallel clients restart from W_start (the first one is loaded);
+      // chained ones keep the registers.  The prox anchor is the start (tools.py:180).
+      if (!P.chained && gs > 0) {
+        (void)load_start();
+        if (lane == 0) { wred[w][0] = 0.f; wred[w][1] = nw0; }
+      } else if (lane == 0) {
+        wred[w][0] = 0.f;                         // ||W - W_a|| = 0 at the new anchor
+      }
+      if (PROX) {
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) lab[par][rt * 16 + l16] = lb[rt];
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ar[i][q] = wr[i][q];
+      }
+      lsum = 0.0;
+    }
+    {
+      SP_STAMP(0)
+      const int e = st / nbat, s = st - e * nbat;
+      const int b0 = s * B, bc = min(B, n - b0);
+      const int par = gs & 1;
+      const unsigned tag32 = gs + 1u;
+      if (w == 0 && lg == 0)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) lab[par][rt * 16 + l16] = lb[rt];
 
-    // ---------------- forward partial: z_g = X_slice W_slice^T (registers only) ----------------
-    floatx4 acc[RT];
+      // ---------------- forward partial: z_g = X_slice W_slice^T (registers only) ----------------
+      floatx4 acc[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < TPW; ++i)
-      if (w + NW * i < NTS)
+      for (int i = 0; i < TPW; ++i)
+        if (w + NW * i < NTS)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+          for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4)
+            for (int e4 = 0; e4 < 4; ++e4)
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xf[i][rt][q], e4), comp(wr[i][q], e4), acc[rt]);
+              for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xf[i][rt][q], e4), comp(wr[i][q], e4), acc[rt]);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
-    SP_STAMP(1)
-    lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
-    SP_STAMP(2)
+        for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
+      SP_STAMP(1)
+      lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
+      SP_STAMP(2)
 
-    // image write: the backward of this step reads the slice from LDS
+      // image write: the backward of this step reads the slice from LDS
 #define SP_IMG_WRITE()                                                               \
   {                                                                                  \
     _Pragma("unroll") for (int i = 0; i < TPW; ++i)                                  \
@@ -218,189 +336,192 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           _Pragma("unroll") for (int q = 0; q < 4; ++q)                              \
             st4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg), xf[i][rt][q]); \
   }
-    // next step's slice into the (now free) registers, then the entry after it
-// which waves issue the next slice's loads right after the hand-off (the others issue
-// them after the softmax, so one wave of each SIMD computes while its partner is held up
-// issuing loads)
-#ifndef SP_LOAD_EARLY
-#define SP_LOAD_EARLY(w_) ((w_) < SP_WAVES / 2)
-#endif
-#ifdef FS_NOLOAD
-#define SP_NEXT_COND false
-#else
-#define SP_NEXT_COND more
-#endif
+      // the next step's slice into the (now free) registers, then the row indices after it.
+      // Half of the waves issue those loads right after the hand-off, half after the
+      // softmax, so one wave of each SIMD computes while its partner is held up issuing loads.
 #define SP_NEXT()                                                                    \
-  if (SP_NEXT_COND) {                                                                \
+  if (lc_ok) {                                                                       \
     SP_XLOAD();                                                                      \
-    if (st + 2 < steps)                                                              \
-      _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) pn[rt] = perm[pos_of(st + 2, rt * 16 + l16)]; \
+    lc_ok = sp_advance(lc, P, grp, ng, T);                                           \
+    if (lc_ok) fetch_rows();                                                         \
   }
 
-    {
-      // ---- hand-off, spread over the waves: wave w owns the values 64 (w + NW m) + lane
-      // (logits, then the two norms).  Guideline 16, R2 form: every value travels as one
-      // 8-byte {tag, value} granule written by ONE relaxed agent-scope (sc1) store -- the
-      // data is its own flag; the partner's granules are re-read with sc1 loads until every
-      // tag equals this step's tag: one round trip once the data is there, no separate flag,
-      // no fences.  Tag = launch generation (high half) | step + 1 (low half), so granules of
-      // an earlier launch never match and the buffer needs no clearing between launches.
-      // The polls are issued before the image write and the next slice's loads are issued
-      // after the check, so the round trip neither queues behind nor waits for them.
-      constexpr int M = (NZ + 2 + 64 * NW - 1) / (64 * NW);
-      unsigned long long* slot = xb + ((int64_t)par * G) * X.SZ;
-      const unsigned long long tag = (unsigned long long)tag32 << 32;
-      float own[M];
-      unsigned long long pl[M][G];
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int idx = 64 * (w + NW * m) + lane;
-        float v = 0.f;
-        if (idx < NZ) {
-          const int r = idx / NC, c = idx - r * NC;
-#pragma unroll
-          for (int i = 0; i < NW; ++i) v += zpart[i][r][c];
-        } else if (idx < NZ + 2) {
-#pragma unroll
-          for (int i = 0; i < NW; ++i) v += wred[i][idx - NZ];
-        }
-        own[m] = v;
-        if (idx < NZ + 2)
-          __hip_atomic_store(slot + (int64_t)g * X.SZ + idx, tag | __float_as_uint(v), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      SP_STAMP(3)
-      auto poll = [&]() {
+      {
+        // ---- hand-off, spread over the threads: thread t owns the values t + 512 m
+        // (the B x C real logits row-major, then the two norms).  Guideline 16, R2 form:
+        // every value travels as one 8-byte {tag, value} granule written by ONE relaxed
+        // agent-scope (sc1) store -- the data is its own flag; the partners' granules are
+        // re-read with sc1 loads until every tag equals this step's tag.  The polls are
+        // issued before the image write and the next slice's loads are issued after the
+        // check, so the round trip neither queues behind nor waits for them.
+        unsigned long long* slot = xb + ((int64_t)par * G) * X.SZ;
+        const unsigned long long tag = (unsigned long long)tag32 << 32;
+        float own[M];
+        unsigned long long pl[M][G];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const int idx = 64 * (w + NW * m) + lane;
-#pragma unroll
-          for (int h = 0; h < G; ++h)
-            pl[m][h] = __hip_atomic_load(slot + (int64_t)h * X.SZ + (idx < NZ + 2 ? idx : 0), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        }
-      };
-      poll();
-      SP_IMG_WRITE();
-      unsigned spins = 0;
-      for (;;) {
-        bool ok = true;
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-#pragma unroll
-          for (int h = 0; h < G; ++h)
-            ok &= (h == g) | (64 * (w + NW * m) + lane >= NZ + 2) | ((unsigned)(pl[m][h] >> 32) == tag32);
-        if (__all(ok)) break;
-        if (++spins > SP_SPIN_LIMIT) {
-          if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        poll();
-      }
-      // sum in slice order 0..G-1 (own partial at position g): identical bits in every partner
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const int idx = 64 * (w + NW * m) + lane;
-        if (idx < NZ + 2) {
+          const int idx = tid + SP_THREADS * m;
           float v = 0.f;
+          if (idx < NV - 2) {
+            const int r = idx / C, c = idx - r * C;
 #pragma unroll
-          for (int h = 0; h < G; ++h) v += (h == g) ? own[m] : __uint_as_float((unsigned)pl[m][h]);
-          if (idx < NZ) (&zsum[0][0])[idx] = v;
-          else nrm[idx - NZ] = v;                // ||W - W_a||^2, ||W||^2 at the start of this step
+            for (int i = 0; i < NW; ++i) v += zpart[i][r][c];
+          } else if (idx < NV) {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) v += wred[i][idx - (NV - 2)];
+          }
+          own[m] = v;
+          if (idx < NV)
+            __hip_atomic_store(slot + (int64_t)g * X.SZ + idx, tag | __float_as_uint(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
-      }
-      SP_STAMP(4)
-      if (SP_LOAD_EARLY(w)) SP_NEXT();
-    }
-    SP_STAMP(5)
-    lds_barrier();  // S2: summed logits and norms, the image
-    SP_STAMP(6)
-    const float invb = 1.0f / (float)bc;
-    float cep = 0.f;
-    for (int idx = tid; idx < NZ; idx += SP_THREADS) {   // NC lanes of one wave hold one row
-      const int r = idx / NC, c = idx - r * NC;
-      const float z = zsum[r][c];
-      const bool valid = r < bc && c < C;
-      float m = valid ? z : -INFINITY;
+        SP_STAMP(3)
+        auto poll = [&]() {
 #pragma unroll
-      for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-      float se = valid ? expf(z - m) : 0.f;
+          for (int m = 0; m < M; ++m) {
+            const int idx = tid + SP_THREADS * m;
 #pragma unroll
-      for (int off = NC / 2; off > 0; off >>= 1) se += __shfl_xor(se, off, 64);
-      float gv = 0.f;
-      if (valid) {
-        const float lp = z - m - logf(se);
-        const bool isy = c == lab[par][r];
-        gv = (isy ? -invb : 0.f) + expf(lp) * invb;
-        if (isy) cep -= lp;
-      }
-      gbuf[r][c] = gv;
-    }
-    cep = wave_sum(cep);
-    if (lane == 0) wce[w] = cep;
-    lds_barrier();  // S3: g, CE partials
-    if (!SP_LOAD_EARLY(w)) SP_NEXT();
-    SP_STAMP(7)
-    const float pn2 = nrm[0], wn2 = nrm[1];
-    if (g == 0 && tid == 0 && e == E - 1) {
-      float ce = 0.f;
-      for (int i = 0; i < NW; ++i) ce += wce[i];
-      float loss = ce / (float)bc;
-      if (P.prox) loss = loss + P.mu * sqrtf(pn2);
-      if (P.reg) loss = loss + P.lam * sqrtf(wn2);
-      lsum += (double)loss * (double)bc;
-    }
-
-    // ---------------- backward + update of the register-resident slice ----------------
-    // A operand lane (l16, lg): image row 4 kk + lg, block 4 (l16 & 3) + (l16 >> 2), so the
-    // output register q of lane (c, lg) is the gradient of d = 16 q + 4 lg + e (the lane's W).
-    float gB[4 * RT];
+            for (int h = 0; h < G; ++h)
+              pl[m][h] = __hip_atomic_load(slot + (int64_t)h * X.SZ + (idx < NV ? idx : 0), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+          }
+        };
+        poll();
+        SP_IMG_WRITE();
+        if (X.spin_limit == 0 && gs == 0 && lane == 0)      // test knob: report an injected timeout
+          __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        for (;;) {
+          bool ok = true;
 #pragma unroll
-    for (int kk = 0; kk < 4 * RT; ++kk) gB[kk] = gbuf[4 * kk + lg][l16];
-    const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;
-    const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
-    const float lr = P.lr;
-    const int rblk = 4 * (l16 & 3) + (l16 >> 2);
-    float npn = 0.f, nwn = 0.f;
+          for (int m = 0; m < M; ++m)
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      const int Tl = w + NW * i;
-      if (Tl < NTS) {
-        floatx4 ga[4];
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) ga[e4] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 4 * RT; ++kk) {
-          const float4 x = ld4(xs_lds + img_off(4 * kk + lg, RS, Tl, rblk));
-#pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
+            for (int h = 0; h < G; ++h)
+              ok &= (h == g) | (tid + SP_THREADS * m >= NV) | ((unsigned)(pl[m][h] >> 32) == tag32);
+          if (__all(ok)) break;
+          if (dead || ++spins > X.spin_limit) {
+            if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dead = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          poll();
         }
-        if (l16 < C) {
+        // sum in slice order 0..G-1 (own partial at position g): identical bits in every partner
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float o[4];
+        for (int m = 0; m < M; ++m) {
+          const int idx = tid + SP_THREADS * m;
+          if (idx < NV) {
+            float v = 0.f;
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) {
-              const float wc = comp(wr[i][q], e4);
-              const float ac = PROX ? comp(ar[i][q], e4) : 0.f;
-              float gr = ga[e4][q];
-              if (PROX) gr = gr + (wc - ac) * sp;
-              if (P.reg) gr = gr + wc * sr;
-              o[e4] = wc - lr * gr;
-              const float dp = o[e4] - ac;
-              npn += dp * dp;
-              nwn += o[e4] * o[e4];
+            for (int h = 0; h < G; ++h) v += (h == g) ? own[m] : __uint_as_float((unsigned)pl[m][h]);
+            if (idx < NV - 2) {
+              const int r = idx / C, c = idx - r * C;
+              zsum[r][c] = v;
+            } else {
+              nrm[idx - (NV - 2)] = v;            // ||W - W_a||^2, ||W||^2 at the start of this step
             }
-            wr[i][q] = make_float4(o[0], o[1], o[2], o[3]);
+          }
+        }
+        SP_STAMP(4)
+        if (w < NW / 2) SP_NEXT();
+      }
+      SP_STAMP(5)
+      lds_barrier();  // S2: summed logits and norms, the image
+      SP_STAMP(6)
+      const float invb = 1.0f / (float)bc;
+      float cep = 0.f;
+      for (int idx = tid; idx < NZ; idx += SP_THREADS) {   // NC lanes of one wave hold one row
+        const int r = idx / NC, c = idx - r * NC;
+        const bool valid = r < bc && c < C;
+        const float z = valid ? zsum[r][c] : 0.f;
+        float m = valid ? z : -INFINITY;
+#pragma unroll
+        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        float se = valid ? expf(z - m) : 0.f;
+#pragma unroll
+        for (int off = NC / 2; off > 0; off >>= 1) se += __shfl_xor(se, off, 64);
+        float gv = 0.f;
+        if (valid) {
+          const float lp = z - m - logf(se);
+          const bool isy = c == lab[par][r];
+          gv = (isy ? -invb : 0.f) + expf(lp) * invb;
+          if (isy) cep -= lp;
+        }
+        gbuf[r][c] = gv;
+      }
+      cep = wave_sum(cep);
+      if (lane == 0) wce[w] = cep;
+      lds_barrier();  // S3: g, CE partials
+      if (w >= NW / 2) SP_NEXT();
+      SP_STAMP(7)
+      const float pn2 = nrm[0], wn2 = nrm[1];
+      if (g == 0 && tid == 0 && e == E - 1) {
+        float ce = 0.f;
+        for (int i = 0; i < NW; ++i) ce += wce[i];
+        float loss = ce / (float)bc;
+        if (P.prox) loss = loss + P.mu * sqrtf(pn2);
+        if (P.reg) loss = loss + P.lam * sqrtf(wn2);
+        lsum += (double)loss * (double)bc;
+      }
+
+      // ---------------- backward + update of the register-resident slice ----------------
+      // A operand lane (l16, lg): image row 4 kk + lg, block 4 (l16 & 3) + (l16 >> 2), so the
+      // output register q of lane (c, lg) is the gradient of d = 16 q + 4 lg + e (the lane's W).
+      float gB[4 * RT];
+#pragma unroll
+      for (int kk = 0; kk < 4 * RT; ++kk) gB[kk] = gbuf[4 * kk + lg][l16];
+      const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;
+      const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
+      const float lr = P.lr;
+      const int rblk = 4 * (l16 & 3) + (l16 >> 2);
+      float npn = 0.f, nwn = 0.f;
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int Tl = w + NW * i;
+        if (Tl < NTS) {
+          floatx4 ga[4];
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) ga[e4] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < 4 * RT; ++kk) {
+            const float4 x = ld4(xs_lds + img_off(4 * kk + lg, RS, Tl, rblk));
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
+          }
+          if (l16 < C) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float o[4];
+#pragma unroll
+              for (int e4 = 0; e4 < 4; ++e4) {
+                const float wc = comp(wr[i][q], e4);
+                const float ac = PROX ? comp(ar[i][q], e4) : 0.f;
+                float gr = ga[e4][q];
+                if (PROX) gr = gr + (wc - ac) * sp;
+                if (P.reg) gr = gr + wc * sr;
+                o[e4] = wc - lr * gr;
+                const float dp = o[e4] - ac;
+                npn += dp * dp;
+                nwn += o[e4] * o[e4];
+              }
+              wr[i][q] = make_float4(o[0], o[1], o[2], o[3]);
+            }
           }
         }
       }
+      npn = wave_sum(npn);
+      nwn = wave_sum(nwn);
+      if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
+      SP_STAMP(8)
     }
-    npn = wave_sum(npn);
-    nwn = wave_sum(nwn);
-    if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
-    SP_STAMP(8)
+    if (st == cc.steps - 1) {                     // client end
+      store_w(P.W_out + (int64_t)cc.j * C * ld);
+      if (g == 0 && tid == 0) P.loss[cc.j] = lsum / (double)n;
+    }
+    const int kprev = cc.k;
+    cc_ok = sp_advance(cc, P, grp, ng, T);
+    flush_empty(kprev + 1, cc_ok ? cc.k : T);
   }
 #undef SP_XLOAD
 #undef SP_IMG_WRITE
@@ -408,18 +529,9 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #ifdef FS_STAMPS
   if (tid == 0 && X.stamps) {
     for (int k = 0; k < 8; ++k) X.stamps[blockIdx.x * 16 + k] = stamp_acc[k];
-    X.stamps[blockIdx.x * 16 + 15] = (unsigned long long)steps;
+    X.stamps[blockIdx.x * 16 + 15] = (unsigned long long)gs;
   }
 #endif
-
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int Tl = w + NW * i;
-    if (Tl < NTS && l16 < C)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) st4(Wj + (int64_t)l16 * ld + 64 * (t0 + Tl) + 16 * q + 4 * lg, wr[i][q]);
-  }
-  if (g == 0 && tid == 0) P.loss[j] = lsum / (double)n;
 }
 
 static int g_cus = 0;
@@ -443,68 +555,84 @@ static size_t split_static_lds(int RT) {
   return (size_t)SP_WAVES * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + SP_WAVES * 3 * 4 + 8 + 64;
 }
 
-// tiles per wave the register budget allows without spilling (slice + weights + anchor)
-static int split_tpw_max(int RT, int G) { return (RT == 2 && G == 4) ? 1 : 2; }
+static int split_rt(int B) { return B <= 16 ? 1 : 2; }
 
-static bool split_fits(int RT, int NT, int G) {
+// can G workgroups split one client of this shape?
+static bool split_fits(int C, int B, int NT, int G) {
+  if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
+  if (C > 16 || B > 32 || NT < G) return false;
+  const int RT = split_rt(B);
   const int tiles = (NT + G - 1) / G;
-  return (tiles + SP_WAVES - 1) / SP_WAVES <= split_tpw_max(RT, G) &&
-         split_dyn_lds(RT, NT, G) + split_static_lds(RT) <= 160 * 1024;
+  if ((tiles + SP_WAVES - 1) / SP_WAVES > SP_TPW) return false;
+  if (G >= 8 && RT * 16 * C + 2 > SP_THREADS) return false;   // one exchanged value per thread
+  return split_dyn_lds(RT, NT, G) + split_static_lds(RT) <= 160 * 1024;
 }
 
-static int64_t split_ws_bytes(int N, int G, int RT) {
-  const int SZ = RT * 16 * 16 + 4;
-  return 256 + (int64_t)N * 2 * G * SZ * 8;
+static int split_sz(int RT) { return RT * 16 * 16 + 4; }
+
+static int split_groups(int N, int G, int chained, int cus) {
+  return chained ? 1 : std::max(1, std::min(N, cus / G));
 }
 
-static unsigned next_generation() {
-  static std::atomic<unsigned> counter{0};
-  return 1u + counter.fetch_add(1u, std::memory_order_relaxed) % 65535u;
+static int64_t split_xbuf_bytes(int ngroups, int G, int RT) { return (int64_t)ngroups * 2 * G * split_sz(RT) * 8; }
+
+static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus) {
+  const int RT = split_rt(B);
+  return split_xbuf_bytes(split_groups(N, G, chained, cus), G, RT) + SP_ERR_BYTES;
 }
 
-template <int RT, int G, int TPW, bool PROX>
-static void launch_split_p(const LTParams& P, const SplitWS& X, size_t lds, hipStream_t st) {
+static unsigned split_spin_limit() {
+  const char* s = getenv("FS_SPIN_LIMIT");        // test knob: 0 injects a hand-off timeout
+  return s ? (unsigned)strtoul(s, nullptr, 10) : SP_SPIN_LIMIT;
+}
+
+template <int RT, int G, bool PROX>
+static void launch_split_p(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, TPW, PROX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, TPW, PROX>), dim3(P.N * G), dim3(SP_THREADS), lds, st, P, X);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
 }
 
-template <int RT, int G, int TPW>
-static void launch_split_t(const LTParams& P, const SplitWS& X, size_t lds, hipStream_t st) {
-  if (P.prox) launch_split_p<RT, G, TPW, true>(P, X, lds, st);
-  else launch_split_p<RT, G, TPW, false>(P, X, lds, st);
+template <int RT, int G>
+static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if (P.prox) launch_split_p<RT, G, true>(P, X, grid, lds, st);
+  else launch_split_p<RT, G, false>(P, X, grid, lds, st);
 }
 
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
-  const int RT = P.B <= 16 ? 1 : 2;
+  const int RT = split_rt(P.B);
   const int NT = (int)(P.ld >> 6);
-  if (!(G == 2 || G == 4)) return fail(FS_EINVAL, "fs_local_train: G must be 1, 2 or 4");
+  if (!(G == 2 || G == 4 || G == 8 || G == 16)) return fail(FS_EINVAL, "fs_local_train: G must be 1, 2, 4, 8 or 16");
   if (P.C > 16 || P.B > 32) return fail(FS_EUNSUPPORTED, "fs_local_train: split clients need C <= 16, B <= 32");
   if (NT < G) return fail(FS_EUNSUPPORTED, "fs_local_train: fewer feature tiles than workgroups per client");
-  if (!ws || ws_bytes < split_ws_bytes(P.N, G, RT)) return fail(FS_EINVAL, "fs_local_train: workspace too small");
+  if (!split_fits(P.C, P.B, NT, G)) return fail(FS_EUNSUPPORTED, "fs_local_train: slice too wide for one workgroup");
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
-  if (!split_fits(RT, NT, G)) return fail(FS_EUNSUPPORTED, "fs_local_train: slice too wide for one workgroup");
-  if (P.N * G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: N*G workgroups exceed the CU count");
-  const size_t lds = split_dyn_lds(RT, NT, G);
-  const int tiles = (NT + G - 1) / G;
-  const int tpw = (tiles + SP_WAVES - 1) / SP_WAVES;
+  if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");
+  const int ng = split_groups(P.N, G, P.chained, cus);
+  const int64_t xbytes = split_xbuf_bytes(ng, G, RT);
+  if (!ws || ws_bytes < xbytes + SP_ERR_BYTES) return fail(FS_EINVAL, "fs_local_train: workspace too small");
   char* base = reinterpret_cast<char*>(ws);
   SplitWS X;
-  X.err = reinterpret_cast<unsigned*>(base);
-  X.xbuf = reinterpret_cast<unsigned long long*>(base + 256);
-  X.G = G;
-  X.SZ = RT * 16 * 16 + 4;
-  X.gen = next_generation();
+  X.xbuf = reinterpret_cast<unsigned long long*>(base);
+  X.err = reinterpret_cast<unsigned*>(base + ws_bytes - SP_ERR_BYTES);   // last block: sticky
+  X.SZ = split_sz(RT);
+  X.ngroups = ng;
+  X.spin_limit = split_spin_limit();
   X.stamps = nullptr;
 #ifdef FS_STAMPS
-  X.stamps = reinterpret_cast<unsigned long long*>(base + ws_bytes - (int64_t)P.N * G * 16 * 8);
+  X.stamps = reinterpret_cast<unsigned long long*>(base + xbytes);
 #endif
-#define FS_SPLIT_CASE(rt, g, tp) \
-  if (RT == rt && G == g && tpw <= tp) { launch_split_t<rt, g, tp>(P, X, lds, st); return FS_OK; }
-  FS_SPLIT_CASE(2, 2, 1) FS_SPLIT_CASE(2, 2, 2) FS_SPLIT_CASE(2, 4, 1)
-  FS_SPLIT_CASE(1, 2, 1) FS_SPLIT_CASE(1, 2, 2) FS_SPLIT_CASE(1, 4, 1) FS_SPLIT_CASE(1, 4, 2)
+  // hand-off tags restart at 1 every launch: clear the exchange granules
+  hipError_t e = hipMemsetAsync(base, 0, (size_t)xbytes, st);
+  if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
+  const size_t lds = split_dyn_lds(RT, NT, G);
+  const int grid = P.chained ? 8 * G : ng * G;
+#define FS_SPLIT_CASE(rt, g) \
+  if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, grid, lds, st); return FS_OK; }
+  FS_SPLIT_CASE(2, 2) FS_SPLIT_CASE(2, 4) FS_SPLIT_CASE(2, 8) FS_SPLIT_CASE(2, 16)
+  FS_SPLIT_CASE(1, 2) FS_SPLIT_CASE(1, 4) FS_SPLIT_CASE(1, 8) FS_SPLIT_CASE(1, 16)
 #undef FS_SPLIT_CASE
   return fail(FS_EUNSUPPORTED, "fs_local_train: no split kernel for this shape");
 }
@@ -513,28 +641,44 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
 
 using namespace fs;
 
-// Plan the launch: G = workgroups per client (1 = one workgroup walks the client; 2 or 4 =
-// split clients) and the workspace bytes it needs.  max_en = max_j E * n_j (unused since
-// the shuffle indices are streamed; kept for the ABI).  The caller zeroes the workspace
-// once at allocation; launches never clear it (hand-off tags carry a launch generation).
+// Plan the launch: G = workgroups per client (1 = one workgroup walks each client; 2..16 =
+// a group of G workgroups splits the feature dimension of one client at a time) and the
+// workspace bytes it needs.  On entry *G_out is a request: 0 = let the planner choose,
+// 1 = one workgroup per client, 2..16 = that group width if the shape allows it (else the
+// planner's choice).  FS_SPLIT_G in the environment overrides a 0 request (diagnostics).
+// max_en = max_j E * n_j.
 extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained,
                                    int* G_out, int64_t* ws_bytes_out) {
   FS_REQUIRE(G_out && ws_bytes_out, "null pointer");
-  FS_REQUIRE(N >= 1 && ld >= 64 && ld % 64 == 0, "bad sizes");
-  (void)max_en;
+  FS_REQUIRE(N >= 1 && B >= 1 && ld >= 64 && ld % 64 == 0, "bad sizes");
+  int want = *G_out;
   *G_out = 1;
   *ws_bytes_out = 0;
+  if (want == 0)
+    if (const char* s = getenv("FS_SPLIT_G")) want = atoi(s);
   const int cus = device_cus();
-  if (chained || C > 16 || B > 32 || cus <= 0) return FS_OK;
-  const int RT = B <= 16 ? 1 : 2;
+  if (want == 1 || C > 16 || B > 32 || cus <= 0) return FS_OK;
   const int NT = (int)(ld >> 6);
-  const int64_t max_steps = (int64_t)E * ((max_en / (E > 0 ? E : 1) + B - 1) / B);
-  if (max_steps >= 65535) return FS_OK;          // hand-off tags hold the step in 16 bits
-  for (int G : {4, 2}) {
-    if (NT < G || N * G > cus || !split_fits(RT, NT, G)) continue;
-    *G_out = G;
-    *ws_bytes_out = split_ws_bytes(N, G, RT) + 4096;
-    return FS_OK;
+  int G = (want > 1 && split_fits(C, B, NT, want) && want <= cus) ? want : 0;
+  if (G == 0) {
+    if (chained) {
+      // one group walks the chain: slice one step's batch (B x ld floats) to ~32 KB per CU
+      const int64_t bytes = (int64_t)B * ld * 4;
+      for (int cand : {2, 4, 8, 16})
+        if (split_fits(C, B, NT, cand) && cand <= cus) {
+          G = cand;
+          if (bytes / cand <= 32 * 1024) break;
+        }
+    } else {
+      // parallel clients: the narrowest group that fits (most clients in flight, fewest partners)
+      for (int cand : {2, 4, 8, 16})
+        if (split_fits(C, B, NT, cand) && cand <= cus) { G = cand; break; }
+    }
   }
+  (void)max_en;
+  (void)E;
+  if (G == 0) return FS_OK;
+  *G_out = G;
+  *ws_bytes_out = split_ws_bytes(N, G, B, chained, cus);
   return FS_OK;
 }

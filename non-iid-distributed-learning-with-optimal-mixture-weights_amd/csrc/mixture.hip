@@ -584,7 +584,8 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
                                                                  float* __restrict__ p, float* __restrict__ buf,
                                                                  int* __restrict__ first_flag,
                                                                  unsigned long long* __restrict__ xbuf,
-                                                                 unsigned* __restrict__ err, int K) {
+                                                                 unsigned* __restrict__ err, int K,
+                                                                 unsigned spin_limit) {
   static_assert(S == 8 || S == 16 || S == 32 || S == 64, "slice width");
   if (blockIdx.x % MC_XCDS) return;
   constexpr int LPV = 64 / S;                      // lanes per value after the reduce-scatter
@@ -629,6 +630,8 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
     vnext = row_at(1);
   }
   bool dead = false;
+  if (spin_limit == 0 && k == 0 && t == 0 && total > 0)   // test knob: report an injected timeout
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   lds_barrier();
   for (int st = 0; st < total; ++st) {
     // ---- next step's slice streams behind this step ----
@@ -670,7 +673,7 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
         for (int q = 0; q < MC_KMAX; ++q)
           if (q < K) ok = ok && (unsigned)(gr[q] >> 32) == tag;
         if (ok || dead) break;
-        if (++spins > MC_SPIN_LIMIT) {
+        if (++spins > spin_limit) {
           dead = true;
           __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -723,22 +726,15 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
   if (k == 0 && t == 0 && total > 0) *first_flag = 0;
 }
 
-// per-device exchange workspace of the multi-CU solver: [2][MC_KMAX][MC_SLOT] granules + error word
-static unsigned long long* g_mc_ws[64];
+// caller-owned workspace of the multi-CU solver: [2][K][MC_SLOT] exchange granules (zeroed
+// before every launch) followed by a 256-byte error block (sticky: only the caller clears it)
+constexpr int64_t MC_ERR_BYTES = 256;
 
-static int mc_workspace(unsigned long long** out) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(FS_EHIP, "fs_mix_solve: no device");
-  if (!g_mc_ws[dev]) {
-    void* q = nullptr;
-    const size_t bytes = sizeof(unsigned long long) * (2 * MC_KMAX * MC_SLOT + 8);
-    hipError_t e = hipMalloc(&q, bytes);
-    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
-    if (hipMemset(q, 0, bytes) != hipSuccess) return fail(FS_EHIP, "fs_mix_solve: workspace memset");
-    g_mc_ws[dev] = reinterpret_cast<unsigned long long*>(q);
-  }
-  *out = g_mc_ws[dev];
-  return FS_OK;
+static int64_t mc_xbytes(int K) { return (int64_t)sizeof(unsigned long long) * 2 * K * MC_SLOT; }
+
+static unsigned mc_spin_limit() {
+  const char* s = getenv("FS_SPIN_LIMIT");        // test knob: 0 injects an exchange timeout
+  return s ? (unsigned)strtoul(s, nullptr, 10) : MC_SPIN_LIMIT;
 }
 
 // slice width for N clients (0: not covered): S clients per workgroup, K = ceil(ldN / S) <= 32
@@ -754,21 +750,27 @@ static int mc_slice(int N) {
   return 0;
 }
 
+static bool mc_covers(int N, int C, int Bv) { return mc_slice(N) != 0 && C <= 16 && Bv <= 16; }
+
 static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
-                        int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+                        int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first, void* d_ws,
+                        int64_t ws_bytes) {
+  if (!mc_covers(N, C, Bv)) return 1;            // not covered
   const int S = mc_slice(N);
-  if (S == 0 || C > 16 || Bv > 16) return 1;     // not covered
   const int K = (mix_ldn(N) + S - 1) / S;
-  unsigned long long* ws = nullptr;
-  if (int rc = mc_workspace(&ws)) return rc;
-  hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned long long) * 2 * K * MC_SLOT, st);
+  const int64_t xbytes = mc_xbytes(K);
+  if (!d_ws || ws_bytes < xbytes + MC_ERR_BYTES)
+    return fail(FS_EINVAL, "fs_mix_solve: workspace too small (see fs_mix_solve_ws_bytes)");
+  unsigned long long* ws = reinterpret_cast<unsigned long long*>(d_ws);
+  unsigned* err = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES);
+  hipError_t e = hipMemsetAsync(ws, 0, (size_t)xbytes, st);
   if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
-  unsigned* err = reinterpret_cast<unsigned*>(ws + 2 * MC_KMAX * MC_SLOT);
+  const unsigned spin_limit = mc_spin_limit();
   const dim3 grid(MC_XCDS * K), block(MC_THREADS);
 #define MC_CASE(S_)                                                                                        \
   if (S == S_)                                                                                             \
     hipLaunchKernelGGL(mix_solve_mc_kernel<S_>, grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, \
-                       buf, first, ws, err, K);
+                       buf, first, ws, err, K, spin_limit);
   MC_CASE(8) MC_CASE(16) MC_CASE(32) MC_CASE(64)
 #undef MC_CASE
   return 0;
@@ -778,13 +780,15 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
 
 using namespace fs;
 
-extern "C" int fs_mix_solve_last_mode(void) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_mc_ws[dev]) return 0;
-  unsigned err = 0;
-  if (hipMemcpy(&err, g_mc_ws[dev] + 2 * MC_KMAX * MC_SLOT, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return 1 | (err ? 4 : 0);
+static thread_local int t_last_solver = 0;
+
+extern "C" int fs_mix_solve_last_mode(void) { return t_last_solver; }
+
+extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
+  if (N < 1) return MC_ERR_BYTES;
+  const int S = mc_slice(N);
+  const int K = S ? (mix_ldn(N) + S - 1) / S : 0;
+  return (mc_covers(N, C, Bv) ? mc_xbytes(K) : 0) + MC_ERR_BYTES;
 }
 
 extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val, float* d_Z,
@@ -802,7 +806,7 @@ extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, 
 
 extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                             int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
-                            int* d_first, void* stream) {
+                            int* d_first, void* d_ws, int64_t ws_bytes, void* stream) {
   FS_REQUIRE(N >= 1 && C >= 1 && n_val >= 1 && epochs >= 0, "bad sizes");
   FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
   FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
@@ -816,13 +820,16 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
   if ((want == "auto" || want == "reg") &&
       mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
+    t_last_solver = 1;
     FS_LAUNCH_CHECK();
     return FS_OK;
   }
   if (want == "auto" || want == "mc") {
-    const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
+    const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
+                                d_first, d_ws, ws_bytes);
     if (rc < 0) return rc;
     if (rc == 0) {
+      t_last_solver = 2;
       FS_LAUNCH_CHECK();
       return FS_OK;
     }
@@ -839,6 +846,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
       }
       hipLaunchKernelGGL(mix_solve_staged_kernel<16>, dim3(1), dim3(MS_THREADS), lds2, st0, d_Z, d_labels, d_perms, N,
                          C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
+      t_last_solver = 3;
       FS_LAUNCH_CHECK();
       return FS_OK;
     }
@@ -853,6 +861,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   }
   hipLaunchKernelGGL(mix_solve_kernel, dim3(1), dim3(MS_THREADS), lds, st, d_Z, d_labels, d_perms, N, C, n_val,
                      epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
+  t_last_solver = 4;
   FS_LAUNCH_CHECK();
   return FS_OK;
 }

@@ -117,12 +117,25 @@ class Shuffler:
         return self.acquire(slot)
 
 
+def _check_ws_error(ws, what):
+    """Read (synchronising) and clear the sticky error word at the start of the workspace's
+    last 256-byte block (include/fedsim.h); raise if a bounded cross-workgroup wait timed out."""
+    if ws is None:
+        return
+    blk = ws[ws.numel() - _lib.ERR_BLOCK:]
+    err = int(blk[:4].view(torch.int32).item())
+    if err:
+        blk.zero_()
+        raise _lib.FedsimError('%s: a cross-workgroup hand-off timed out (code %d); results are invalid' % (what, err))
+
+
 class LocalTrainer:
     """fs_local_train for a fixed set of clients; owns the clients x params buffer.
 
-    ``split``: workgroups per client.  None asks fs_local_train_plan (split clients when the
-    round has fewer clients than CUs and the shape allows it, parallel mode only); 1 forces
-    one workgroup per client."""
+    ``split``: workgroups per client.  None asks fs_local_train_plan (a group of G
+    workgroups splits each client's feature dimension whenever the shape allows, in parallel
+    mode as persistent groups over the clients, in chained mode as one group walking the
+    chain); 1 forces one workgroup per client."""
 
     def __init__(self, feats, C, B, E, split=None, chained=False):
         self.f = feats
@@ -130,6 +143,7 @@ class LocalTrainer:
         dev = feats.device
         N = len(feats.ns)
         self.N = N
+        self.chained = bool(chained)
         self.W_out = torch.empty(N, self.C, feats.ld, device=dev, dtype=torch.float32)
         self.loss = torch.zeros(N, device=dev, dtype=torch.float64)
         # pass p = j*E + e  ->  (n_j, offset)
@@ -142,16 +156,16 @@ class LocalTrainer:
         order = np.argsort(-steps, kind='stable').astype(np.int32)     # LPT: longest clients dispatched first
         self.order = torch.from_numpy(order).to(dev)
         import ctypes
-        g, wsb = ctypes.c_int(1), ctypes.c_int64(0)
-        if split != 1 and not chained:
-            max_en = int(self.E * ns.max()) if N else 0
-            _lib.check(_lib.lib().fs_local_train_plan(N, self.C, self.B, self.E, feats.ld, max_en, 0,
-                                                      ctypes.byref(g), ctypes.byref(wsb)), 'fs_local_train_plan')
-            if split is not None:          # explicit G: the launch validates it
-                g.value = int(split)
-                wsb.value = max(int(wsb.value), 1 << 20)
+        g, wsb = ctypes.c_int(0 if split is None else int(split)), ctypes.c_int64(0)
+        max_en = int(self.E * ns.max()) if N else 0
+        _lib.check(_lib.lib().fs_local_train_plan(N, self.C, self.B, self.E, feats.ld, max_en, int(self.chained),
+                                                  ctypes.byref(g), ctypes.byref(wsb)), 'fs_local_train_plan')
+        if split is not None and int(split) != g.value:
+            raise _lib.FedsimError('fs_local_train_plan: G=%d is not available for this shape (planner: %d)'
+                                   % (int(split), g.value))
         self.G = int(g.value)
-        self.ws = torch.zeros(max(256, int(wsb.value)), dtype=torch.uint8, device=dev) if self.G > 1 else None
+        self.ws = (torch.zeros(max(2 * _lib.ERR_BLOCK, int(wsb.value)), dtype=torch.uint8, device=dev)
+                   if self.G > 1 else None)
 
     @property
     def shuffler(self):
@@ -162,10 +176,7 @@ class LocalTrainer:
 
     def check_errors(self):
         """Raise if a split-client launch reported a broken hand-off (synchronises)."""
-        if self.G > 1:
-            err = int(self.ws[:4].view(torch.int32).item())
-            if err:
-                raise _lib.FedsimError('fs_local_train: split-client hand-off failed (code %d)' % err)
+        _check_ws_error(self.ws, 'fs_local_train')
 
     def upload_perms(self, seeds, slot=0, stream=None):
         """seeds: [N*E] sampler seeds of one round's local training passes (client-major);
@@ -293,7 +304,13 @@ class Mixture:
         self.p = p0.to(device=device, dtype=torch.float32).clone()
         self.buf = torch.zeros(self.N, dtype=torch.float32, device=device)
         self.first = torch.ones(1, dtype=torch.int32, device=device)
+        self.ws = torch.zeros(int(_lib.lib().fs_mix_solve_ws_bytes(self.N, self.C, self.Bv)), dtype=torch.uint8,
+                              device=device)
         self.shuffler = None
+
+    def check_errors(self):
+        """Raise if a multi-CU p-solve reported a timed-out exchange (synchronises)."""
+        _check_ws_error(self.ws, 'fs_mix_solve')
 
     def prepare(self, seeds, slot=0, stream=None):
         """Enqueue one round's validation-pass shuffles (one seed per inner epoch)."""
@@ -321,7 +338,7 @@ class Mixture:
         _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(perms), self.N,
                                   self.C, self.nv, epochs, self.Bv, float(lr_p), self.momentum,
                                   _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first),
-                                  _lib.stream_ptr()), 'fs_mix_solve')
+                                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream_ptr()), 'fs_mix_solve')
         self.shuffler.release(slot)
         return self.p
 

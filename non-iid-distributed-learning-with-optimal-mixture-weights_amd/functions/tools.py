@@ -65,7 +65,17 @@ def _device():
     return torch.device('cuda', torch.cuda.current_device())
 
 
-def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round):
+def _check_labels(ys, num_classes, what):
+    """Every label in [0, num_classes): the kernels index class rows by label, and the
+    reference's CrossEntropyLoss raises on an out-of-range target."""
+    for y in ys:
+        y = torch.as_tensor(y)
+        if y.numel() and (int(y.min()) < 0 or int(y.max()) >= num_classes):
+            raise ValueError('%s labels must lie in [0, %d), got [%d, %d]' % (what, num_classes, int(y.min()),
+                                                                              int(y.max())))
+
+
+def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test=None, y_val=None):
     if type != 'classification':
         raise NotImplementedError("only type='classification' is implemented (tools.py:181-184 MSE branch "
                                   "is out of scope)")
@@ -81,6 +91,11 @@ def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round)
         raise NotImplementedError('batch_size must be in [1, 64]')
     if epoch < 1 or round < 0:
         raise ValueError('epoch must be >= 1 and round >= 0')
+    _check_labels(y_train, num_classes, 'training')
+    if y_test is not None:
+        _check_labels([y_test], num_classes, 'test')
+    if y_val is not None:
+        _check_labels([y_val], num_classes, 'validation')
 
 
 class Federation:
@@ -90,9 +105,16 @@ class Federation:
     def __init__(self, algo, X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
                  batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=None, verbose=True,
                  shuffle_device=True):
-        _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round)
+        _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test,
+                      validloader.dataset.tensors[1] if validloader is not None else None)
         if clients not in ('sequential', 'parallel'):
             raise ValueError("clients must be 'sequential' or 'parallel'")
+        self.chained = clients == 'sequential'
+        self.rank, nranks = dist.world()
+        self.sharded = (not self.chained) and nranks > 1
+        if self.sharded and len(y_train) < nranks:
+            raise ValueError("clients='parallel' over %d ranks needs at least one client per rank (got %d clients)"
+                             % (nranks, len(y_train)))
         dev = _device()
         self.algo, self.stats, self.verbose = algo, stats, verbose
         self.C, self.E, self.B, self.R, self.D = int(num_classes), int(epoch), int(batch_size), int(round), int(D)
@@ -102,9 +124,6 @@ class Federation:
         self.N = N
         ns = np.array([len(y) for y in y_train], dtype=np.int64)
         self.ns = ns
-        self.chained = clients == 'sequential'
-        self.rank, nranks = dist.world()
-        self.sharded = (not self.chained) and nranks > 1
         self.shards = dist.shard_lpt(dist.client_work(ns, E, B), nranks) if self.sharded else [np.arange(N)]
         self.mine = self.shards[self.rank] if self.sharded else self.shards[0]
         mine = self.mine
@@ -199,6 +218,8 @@ class Federation:
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""
         R, D = self.t, self.D
         self.trainer.check_errors()
+        if self.mixture is not None:
+            self.mixture.check_errors()
         loss_hist = self.loss_hist[:R]
         if self.sharded:
             loss_hist = dist.allgather_rows(loss_hist.t().contiguous(), [len(s) for s in self.shards]).t()
@@ -261,7 +282,13 @@ def FedAMW(X_train, y_train, X_test, y_test, validloader, type='classification',
 def RFF(d, sigma, D):
     """tools.py:15-19: W ~ N(0, sigma) [d, D], b ~ U(0, 2 pi) [1, D], drawn on torch's global
     CPU generator exactly as the reference draws them (Uniform.sample((1, D)) -> (1, D, 1) ->
-    view), then placed on the GPU."""
+    view), then placed on the GPU.
+
+    RNG stream: this reproduces the reference run on a CPU-only host (device = cpu,
+    tools.py:12), which is what the golden fixtures pin.  On a CUDA/ROCm host the reference
+    draws W and b from the GPU generator instead and leaves the CPU stream untouched, so its
+    later MLP inits and DataLoader shuffles are shifted by these d*D + D draws relative to
+    this drop-in; that GPU-host stream is not reproduced (parity unpinned for it)."""
     m = torch.distributions.Uniform(torch.tensor([0.0]), torch.tensor([2 * torch.pi]))
     W = torch.normal(0, sigma, size=(d, D))
     b = m.sample((1, D)).view(-1, D)
@@ -318,7 +345,7 @@ def Centralized(X_train, y_train, X_test, y_test, type='classification', num_cla
     """tools.py:240-255: every client's rows concatenated (client order), ONE train_loop of
     ``epoch`` epochs (exp.py:116 passes local_epoch * Round), one test_loop.  Returns
     (train_loss, test_loss, test_acc) as Python floats, like the reference's Meter averages."""
-    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0)
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0, y_test)
     dev = _device()
     C = int(num_classes)
     W_init = init_weights(D, C)
@@ -343,7 +370,7 @@ def Distributed(X_train, y_train, X_test, y_test, type='classification', num_cla
     """tools.py:258-276: chained local training of ``epoch`` epochs per client, one
     n_j-weighted aggregate (fs_aggregate, the reference's left fold), one test_loop.  Returns
     (train_loss 0-dim fp32 tensor, test_loss float, test_acc float)."""
-    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0)
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, 0, y_test)
     dev = _device()
     C = int(num_classes)
     W_init = init_weights(D, C)
@@ -382,7 +409,8 @@ def FedAMW_OneShot(X_train, y_train, X_test, y_test, validloader, type='classifi
     a copy of the clients x params buffer; the N-client fold with weight 1 on that row adds
     the rest), bitwise the reference's sequence of roundings.
     Returns (train_loss 0-dim fp32 tensor, test_loss [round], test_acc [round])."""
-    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round)
+    _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test,
+                  validloader.dataset.tensors[1])
     dev = _device()
     C, R = int(num_classes), int(round)
     W_init = init_weights(D, C)
@@ -419,6 +447,7 @@ def FedAMW_OneShot(X_train, y_train, X_test, y_test, validloader, type='classifi
             W_hist[t].copy_(W_g)
         ev.run(W_g, eval_hist[t])
     trainer.check_errors()
+    mix.check_errors()
     train_loss = torch.sum(p0 * torch.tensor([float(v) for v in loss.cpu().numpy()]))   # tools.py:292
     evh = eval_hist[:R].cpu().numpy()
     _print_tests(evh, verbose)

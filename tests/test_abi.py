@@ -39,10 +39,20 @@ def test_abi_version():
     (lambda L: L.fs_local_train_plan(0, 10, 32, 2, 64, 64, 0, None, None), 'null'),
     (lambda L: L.fs_aggregate(None, 64, None, 0, 64, None, None, 0, 1, None), 'N'),
     (lambda L: L.fs_eval(None, 64, None, 0, None, 10, None, None, None), 'n'),
-    (lambda L: L.fs_mix_solve(None, None, None, 5, 3, 10, 1, 65, 0.1, 0.9, None, None, None, None), 'batch'),
+    (lambda L: L.fs_mix_solve(None, None, None, 5, 3, 10, 1, 65, 0.1, 0.9, None, None, None, None, 0, None),
+     'batch'),
 ])
 def test_invalid_arguments_fail_without_touching_the_gpu(call, needle):
     L = _lib.lib()
     rc = call(L)
     assert rc == -1
     assert needle in L.fs_last_error().decode()
+
+
+def test_workspace_sizes_are_host_only():
+    """Workspace queries are pure host arithmetic (no GPU needed) and always leave room for
+    the 256-byte error block at the end."""
+    L = _lib.lib()
+    assert L.fs_mix_solve_ws_bytes(100, 10, 16) >= _lib.ERR_BLOCK
+    assert L.fs_mix_solve_ws_bytes(1000, 10, 16) > L.fs_mix_solve_ws_bytes(10, 2, 16)   # multi-CU granules
+    assert L.fs_mix_solve_last_mode() in _lib.SOLVER_NAMES

@@ -123,18 +123,19 @@ def _rand_clients(rs, sizes, D, C):
     (2048, 10, 32, [512, 100], True, True),               # benchmark width (weights resident in LDS)
     (4000, 10, 32, [70, 33], True, True),                 # weights too large for LDS: global-memory path
 ])
-@pytest.mark.parametrize('mode', ['chained', 'parallel-1wg', 'parallel-auto'])
+@pytest.mark.parametrize('mode', ['chained-1wg', 'chained-auto', 'parallel-1wg', 'parallel-auto'])
 def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, mode):
-    """chained = reference semantics (one workgroup walks the chain); parallel-1wg = one
-    workgroup per client; parallel-auto = the planner's choice (split clients: G=2/4
-    workgroups per client exchanging partial logits, whenever the shape allows)."""
+    """chained = reference semantics (client i starts from client i-1's result); *-1wg = one
+    workgroup per client (chained: one workgroup walks the chain); *-auto = the planner's
+    choice (a group of G workgroups splits each client's features and exchanges partial
+    logits every step, whenever the shape allows; chained: one group walks the chain)."""
     rs = np.random.RandomState(D + C + B)
     Xs, ys = _rand_clients(rs, sizes, D, C)
     W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
     lr, mu, lam, E = 0.4, 0.03, 0.002, 2
-    chained = mode == 'chained'
+    chained = mode.startswith('chained')
     W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=11,
-                             split=1 if mode == 'parallel-1wg' else None)
+                             split=1 if mode.endswith('1wg') else None)
     torch.manual_seed(11)   # the oracle draws the same passes (client-major, epoch-minor)
     start = W0
     for j, (X, y) in enumerate(zip(Xs, ys)):
@@ -144,6 +145,78 @@ def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, mode):
         assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref))
         if chained:
             start = Wr
+
+
+@pytest.mark.parametrize('G', [2, 4, 8, 16])
+@pytest.mark.parametrize('chained', [True, False])
+@pytest.mark.parametrize('prox', [True, False])
+def test_local_train_split_widths(amd, G, chained, prox):
+    """Every group width of the split-client kernel, chained (one group walks the chain) and
+    parallel, against the oracle: D = 1000 (16 tiles, the last one ragged), C = 10, tail
+    batches of 1 and 7 rows, and a client with no rows (its result is its start)."""
+    rs = np.random.RandomState(G + 10 * chained + 100 * prox)
+    D, C, B, E = 1000, 10, 32, 2
+    sizes = [65, 33, 0, 7, 96, 40]
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    lr, mu, lam = 0.4, 0.03, 0.002
+    W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, True, lam, chained, seed=3, split=G)
+    assert _train_via_abi.last_G == G
+    torch.manual_seed(3)
+    start = W0
+    for j, (X, y) in enumerate(zip(Xs, ys)):
+        Wr, lref = O.train_client(X, y, start, lr, E, B, prox, mu, True, lam)
+        assert np.abs(W[j] - Wr).max() <= 2e-5 * max(1.0, np.abs(Wr).max()), (j, np.abs(W[j] - Wr).max())
+        assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
+        if chained:
+            start = Wr
+
+
+@pytest.mark.parametrize('N,G', [(300, 2), (700, 4)])
+def test_local_train_persistent_groups(amd, N, G):
+    """More clients than groups (N * G > CUs): every group walks several clients in the
+    snake order over the LPT list, the next client's first rows streaming in during the
+    previous client's last step.  All clients against the oracle."""
+    rs = np.random.RandomState(N)
+    D, C, B, E = 256, 6, 32, 2
+    sizes = list(rs.randint(1, 90, size=N))
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    W, loss = _train_via_abi(amd, Xs, ys, W0, 0.3, E, B, True, 0.02, True, 0.001, False, seed=9, split=G)
+    torch.manual_seed(9)
+    for j, (X, y) in enumerate(zip(Xs, ys)):
+        Wr, lref = O.train_client(X, y, W0, 0.3, E, B, True, 0.02, True, 0.001)
+        assert np.abs(W[j] - Wr).max() <= 2e-5 * max(1.0, np.abs(Wr).max()), j
+        assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
+
+
+def test_split_handoff_timeout_raises(amd, monkeypatch):
+    """A timed-out partner hand-off is reported, not silently absorbed: FS_SPIN_LIMIT=0 (the
+    test knob) makes the launch set its workspace error word; check_errors raises and clears
+    it, and the next launch is clean."""
+    rs = np.random.RandomState(1)
+    Xs, ys = _rand_clients(rs, [40, 70], 256, 4)
+    W0 = (rs.normal(size=(4, 256)) * 0.1).astype(np.float32)
+    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
+    with pytest.raises(amd.lib.FedsimError, match='timed out'):
+        _train_via_abi(amd, Xs, ys, W0, 0.3, 2, 32, False, 0.0, False, 0.0, False, seed=1, split=2)
+    monkeypatch.delenv('FS_SPIN_LIMIT')
+    _train_via_abi(amd, Xs, ys, W0, 0.3, 2, 32, False, 0.0, False, 0.0, False, seed=1, split=2)
+
+
+def test_mix_solve_timeout_raises(amd, monkeypatch):
+    """Same for the multi-CU p-solve, through the FedAMW drop-in: results() raises
+    FedsimError instead of returning NaN mixture weights."""
+    rs = np.random.RandomState(2)
+    N, D, C = 300, 64, 4
+    Xs, ys = _rand_clients(rs, list(rs.randint(5, 20, size=N)), D, C)
+    Xv = (np.cos(rs.normal(size=(64, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=64).astype(np.int64)
+    T = torch.from_numpy
+    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
+    with pytest.raises(amd.lib.FedsimError, match='fs_mix_solve'):
+        amd.tools.FedAMW([T(x) for x in Xs], [T(y) for y in ys], T(Xv), T(yv), _dl(Xv, yv), 'classification', C,
+                         D, 0.5, 1, 32, False, 0.0, True, 1e-3, 1, 0.01, clients='parallel', verbose=False)
 
 
 def test_aggregate_bitexact_and_chunked(amd):
@@ -205,6 +278,7 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         torch.manual_seed(70 + rnd)
         mix.solve(Wd, amd.rng.draw_pass_seeds(2), lr)
         torch.cuda.synchronize()
+        mix.check_errors()
         torch.manual_seed(70 + rnd)
         pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, lr, 2, batch_size=Bv)
         assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
@@ -232,7 +306,7 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
     # summation orders of the 10^4-term logits drift past 1e-5; the configs use lr_p ~ 1e-3)
     test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)
     mode = amd.lib.lib().fs_mix_solve_last_mode()
-    assert mode == 1, mode             # the multi-CU solver ran, no spin timed out
+    assert mode == 2, mode             # the multi-CU solver ran (a timed-out spin raises in check_errors)
 
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
@@ -365,7 +439,7 @@ def test_fedamw_dropin_many_clients_vs_oracle(amd, N):
     tr, tl, ta = amd.tools.FedAMW([T(x) for x in Xs], [T(y) for y in ys], T(Xt), T(yt), _dl(Xv, yv),
                                   'classification', C, D, 0.5, 2, 32, False, 0.0, True, 1e-3, R, lr_p,
                                   clients='parallel', stats=stats, verbose=False)
-    assert amd.lib.lib().fs_mix_solve_last_mode() == 1     # the multi-CU solver ran, no spin timed out
+    assert amd.lib.lib().fs_mix_solve_last_mode() == 2     # the multi-CU solver ran (results() checks its error word)
     torch.manual_seed(5)
     otr, otl, ota, trace = O.FedAMW(Xs, ys, Xt, yt, Xv, yv, 'classification', C, D, 0.5, 2, 32, False, 0.0, True,
                                     1e-3, R, lr_p, clients='parallel')
