@@ -14,6 +14,7 @@ What it restates (numpy float32, closed-form gradients, one client at a time):
   * ``test_eval``        -- ``test_loop`` + ``comp_accuracy`` + ``Meter``  tools.py:218-237, 82-166 (Q13)
   * ``aggregate``        -- the inline left fold            tools.py:345-350
   * ``mixture_solve``    -- FedAMW's p-SGD                  tools.py:441-453 (Q6, Q7)
+                            (``mixture_solve_z``: the same on precomputed validation logits)
   * ``FedAvg/FedProx/FedAMW`` -- round drivers              tools.py:329-380, 413-463
 
 The RNG stream is torch's own CPU generator (the generator the reference draws
@@ -183,9 +184,17 @@ def mixture_solve(Ws, Xv, yv, p, buf, lr_p, epochs, batch_size=16, momentum=0.9)
     Returns (p, buf).
     """
     Xv = np.asarray(Xv, dtype=F32)
-    yv = np.asarray(yv, dtype=np.int64)
     W3 = np.stack(Ws, axis=0).astype(F32)          # [N, C, D]
     Z = np.einsum('ncd,vd->ncv', W3, Xv, optimize=True).astype(F32)   # [N, C, n_v]
+    return mixture_solve_z(Z, yv, p, buf, lr_p, epochs, batch_size, momentum)
+
+
+def mixture_solve_z(Z, yv, p, buf, lr_p, epochs, batch_size=16, momentum=0.9):
+    """The p-SGD of ``mixture_solve`` on precomputed validation logits Z [N, C, n_v]
+    (tools.py:448 with the inner matmul hoisted, Q7) -- lets a check at large N x D feed the
+    GPU's own Z (itself checked separately) instead of recomputing the D-wide GEMM here."""
+    Z = np.asarray(Z, dtype=F32)
+    yv = np.asarray(yv, dtype=np.int64)
     p = np.array(p, dtype=F32, copy=True)
     lr32, mom32 = F32(lr_p), F32(momentum)
     nv = len(yv)
@@ -407,9 +416,10 @@ def feature_mapping(X_train, X_test, k_par=10, D=200, type='gaussian'):
 
 # --------------------------------------------------------------------------- #
 # exp.py's data preparation -- exp.py:60-99,
-# utils.py:314-349.  Restatements; the reference's utils.py cannot be imported here
-# (top-level torchvision import), so the partitioner is checked by properties and by
-# agreement with the product's host code, not against reference output.
+# utils.py:314-349.  Restatements, pinned to the reference's own output: make_golden.py runs
+# the reference's utils.py (with a torchvision stub) on synthetic LIBSVM files and records
+# the partition, the full-batch order, the splits, feature heads and the heterogeneity
+# (tests/golden/prep_*.npz, checked in tests/test_oracle_prep.py).
 # --------------------------------------------------------------------------- #
 def dirichlet_partition(labels, n_clients, alpha):
     """utils.py:314-349 (psizes = [1/n_clients] * n_clients, exp.py -> utils.py:125)."""
@@ -472,4 +482,4 @@ def exp_prepare(X, y, Xt, yt, n_clients, alpha, k_par, D):
         Xs.append(Xi[r[cut:]])
         ys.append(yi[r[cut:]])
     return dict(parts=parts, X_train=Xs, y_train=ys, X_val=np.concatenate(Xv), y_val=np.concatenate(yv),
-                X_test=te, hete=hete)
+                X_test=te, hete=hete, X_clients=Xc)

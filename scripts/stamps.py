@@ -1,32 +1,61 @@
-"""Diagnostic: per-phase cycle split of the split-client local-training kernel (stamp build).
-Run with FEDSIM_LIB=<pkg>/libfedsim_stamps.so on the GPU box."""
-import os, sys
+"""Diagnostic: per-phase cycle split of the split-client group kernel (stamp build).
+
+    make -C <pkg>/csrc stamps
+    FEDSIM_LIB=<pkg>/libfedsim_stamps.so python scripts/stamps.py --config 5 [--G 16] [--chained]
+
+Wave 0 of every workgroup sums s_memtime deltas per phase over its steps (the stamps cost
+~40 cycles each); printed as cycles per step (mean / min / max over workgroups)."""
+import argparse
+import os
+import sys
+
 import numpy as np
 import torch
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import fedamw_amd
-from fedamw_amd import engine, rng, data
-dev = torch.device('cuda')
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-d = data.federated(N, 512, 2048, 10, 1000, device=dev)
-feats = engine.Features(d['X_train'], d['y_train'], 2048, dev)
-tr = engine.LocalTrainer(feats, 10, 32, 2, split=(int(sys.argv[2]) if len(sys.argv) > 2 else None))
-ws_extra = N * tr.G * 16 * 8
-tr.ws = torch.zeros(tr.ws.numel() + ws_extra, dtype=torch.uint8, device=dev)
-torch.manual_seed(0)
-tr.upload_perms(rng.draw_pass_seeds(N * 2))
-W0 = torch.zeros(10, feats.ld, device=dev)
-for _ in range(3):
-    tr.run(W0, 0.5, False, 0, False, 0, False)
-torch.cuda.synchronize()
-st = tr.ws[-ws_extra:].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
-st = st[st[:, 15] > 0]
-steps = st[:, 15]
-names = (["fwd", "B3", "publish", "img", "doL", "B1", "softmax+B2", "bwd", "-", "check"] if os.environ.get("PAIR") else
-         ["fwd", "S1", "sum+publish", "poll+sum", "img+next", "S2", "softmax+S3", "bwd"])
-per = st[:, :len(names)] / steps[:, None]
-print('G', tr.G, 'blocks', len(st), 'steps', steps[0])
-for k, nm in enumerate(names):
-    print('%-12s mean %8.0f  min %8.0f  max %8.0f cycles/step' % (nm, per[:, k].mean(), per[:, k].min(), per[:, k].max()))
-print('total       mean %8.0f cycles/step' % per.sum(1).mean())
-print('re-polls per step (wave 0): mean %.3f max %.3f' % ((st[:, 11] / steps).mean(), (st[:, 11] / steps).max()))
+import fedamw_amd  # noqa: E402,F401
+from fedamw_amd import data, engine, rng  # noqa: E402
+from scripts.lt_sweep import SHAPES  # noqa: E402
+
+NAMES = ['fwd', 'S1', 'sum+publish', 'poll+sum', 'next(early)', 'S2', 'softmax+S3+next', 'bwd+update']
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', type=int, default=2, choices=sorted(SHAPES))
+    ap.add_argument('--G', type=int, default=0)
+    ap.add_argument('--chained', action='store_true')
+    a = ap.parse_args()
+    assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
+    sh = SHAPES[a.config]
+    chained = a.chained or sh.get('chained', False)
+    dev = torch.device('cuda')
+    N, D, C, E, B = sh['clients'], sh['D'], sh['C'], 2, 32
+    d = data.federated(N, sh['rows'], D, C, 1000, shape=sh['shape'], device=dev)
+    feats = engine.Features(d['X_train'], d['y_train'], D, dev)
+    tr = engine.LocalTrainer(feats, C, B, E, split=(a.G or None), chained=chained)
+    grid = 8 * tr.G if chained else tr.ws.numel() // (2 * tr.G * (16 * 32 + 4) * 8) * tr.G
+    extra = grid * 16 * 8
+    base = tr.ws.numel() - fedamw_amd._lib.ERR_BLOCK          # exchange granules; stamps go right after
+    tr.ws = torch.zeros(tr.ws.numel() + extra, dtype=torch.uint8, device=dev)
+    torch.manual_seed(0)
+    tr.upload_perms(rng.draw_pass_seeds(N * E))
+    W0 = torch.zeros(C, feats.ld, device=dev)
+    for _ in range(3):
+        tr.run(W0, 0.5, False, 0, True, 1e-5, chained)
+    torch.cuda.synchronize()
+    tr.check_errors()
+    st = tr.ws[base:base + extra].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
+    st = st[st[:, 15] > 0]
+    steps = st[:, 15]
+    per = st[:, :len(NAMES)] / steps[:, None]
+    print('config %d G %d (%s): %d workgroups, %.0f steps each' % (a.config, tr.G, 'chained' if chained else
+                                                                   'parallel', len(st), steps.mean()))
+    for k, nm in enumerate(NAMES):
+        print('%-16s mean %8.0f  min %8.0f  max %8.0f cycles/step' % (nm, per[:, k].mean(), per[:, k].min(),
+                                                                       per[:, k].max()))
+    print('total            mean %8.0f cycles/step' % per.sum(1).mean(), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -8,11 +8,20 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 ROUND_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'fed*.npz')))
 TRAIN_UNITS = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'unit_train_*.npz')))
+LONG_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'long_fed*.npz')))
 
 
 def load(name):
     z = np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False)
     return {k: z[k] for k in z.files}
+
+
+def load_long(name):
+    """A long-horizon case: the shared inputs (long_data.npz) merged with the case's
+    hyper-parameters and reference outputs; ``W`` holds the global model at rounds ``snap``."""
+    d = load('long_data')
+    d.update(load(name))
+    return d
 
 
 def split_clients(d):

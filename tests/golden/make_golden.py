@@ -21,6 +21,18 @@ Two client modes are recorded:
 Unit fixtures for one ``train_loop`` call and one ``test_loop`` call are also
 written (``unit_train_*.npz``, ``unit_test.npz``).
 
+Long-horizon fixtures (``long_*.npz``, inputs in ``long_data.npz``): FedProx and FedAMW,
+chained and parallel clients, D = 1024, C = 10, R = 20 rounds (fp32 drift over many
+rounds pinned to the reference; exp.py:31-36 runs D = 2000, R = 100).
+
+Data-preparation fixtures (``prep_*.npz``): exp.py:60-99 run through the reference's own
+``functions/utils.py`` (``load_full_data`` -> ``svmlight_data`` +
+``get_Dirichlet_distribution``) on synthetic LIBSVM files written here, with two
+in-process stand-ins for what this image lacks and that path never uses: a ``torchvision``
+module stub (utils.py:16-19 imports it at top level; only the MNIST/CIFAR branches use it)
+and scipy's removed ``csr_matrix.A`` (utils.py:56) as ``toarray()``.  exp.py's own lines
+61-99 (which call ``iter(loader).next()``, gone in torch 2) are restated below.
+
 The reference's source never leaves this container; only these fixtures do.
 """
 import contextlib
@@ -321,8 +333,159 @@ def run_rff():
         print(name, Xf.shape, Xtf.shape)
 
 
+LONG_R = 20
+LONG_DATA = dict(seed=31, sizes=[150, 97, 64, 33], n_test=100, n_raw=16, D=1024, C=10, val_frac=0.2)
+LONG_SNAP = [0, 4, 9, 14, 19]          # rounds whose global model is stored
+LONG_CASES = [
+    ('long_fedprox_seq', 'fedprox', 'seq', dict(lr=0.5, epoch=2, batch_size=32, prox=True, mu=0.01, reg=True,
+                                                lam=1e-4, R=LONG_R)),
+    ('long_fedprox_par', 'fedprox', 'par', dict(lr=0.5, epoch=2, batch_size=32, prox=True, mu=0.01, reg=True,
+                                                lam=1e-4, R=LONG_R)),
+    ('long_fedamw_seq', 'fedamw', 'seq', dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True,
+                                              lam=1e-4, R=LONG_R, lr_p=0.01)),
+    ('long_fedamw_par', 'fedamw', 'par', dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True,
+                                              lam=1e-4, R=LONG_R, lr_p=0.01)),
+]
+
+
+def run_long():
+    d = synth(**LONG_DATA)
+    np.savez_compressed(os.path.join(OUT, 'long_data.npz'), **d, torch_seed=TORCH_SEED, C=LONG_DATA['C'],
+                        D=LONG_DATA['D'], snap=np.array(LONG_SNAP))
+    Xs, ys, Xt, yt = _split(d)
+    C, D = LONG_DATA['C'], LONG_DATA['D']
+    vl = torch.utils.data.DataLoader(
+        torch.utils.data.TensorDataset(torch.from_numpy(d['X_val']), torch.from_numpy(d['y_val'])),
+        batch_size=16, shuffle=True)
+    for name, algo, mode, hp in LONG_CASES:
+        _trace['W'].clear()
+        _trace['p'].clear()
+        pos = ('classification', C, D, hp['lr'], hp['epoch'], hp['batch_size'], hp['prox'], hp['mu'],
+               hp['reg'], hp['lam'], hp['R'])
+        torch.manual_seed(TORCH_SEED)
+        with contextlib.redirect_stdout(io.StringIO()):
+            if algo == 'fedprox':
+                tr, tl, ta = {'seq': T.FedProx, 'par': _fed_par}[mode](Xs, ys, Xt, yt, *pos)
+            else:
+                tr, tl, ta = {'seq': T.FedAMW, 'par': _fedamw_par}[mode](Xs, ys, Xt, yt, vl, *pos, hp['lr_p'])
+        rec = {k: np.asarray(v) for k, v in hp.items()}
+        rec.update(algo=algo, mode=mode, train_loss=tr.detach().numpy(), test_loss=tl.numpy(), test_acc=ta.numpy(),
+                   W=np.stack(_trace['W'])[LONG_SNAP], snap=np.array(LONG_SNAP))
+        if _trace['p']:
+            rec['p'] = np.stack(_trace['p'])
+        np.savez_compressed(os.path.join(OUT, name + '.npz'), **rec)
+        print(name, 'acc', np.round(ta.numpy()[LONG_SNAP], 2), 'loss', np.round(tr.detach().numpy()[LONG_SNAP], 4))
+
+
+def _reference_utils():
+    """Import /root/reference/functions/utils.py with the two stand-ins described above."""
+    import types
+    import scipy.sparse
+    for m in ('torchvision', 'torchvision.datasets', 'torchvision.transforms', 'torchvision.models'):
+        sys.modules.setdefault(m, types.ModuleType(m))
+    tv = sys.modules['torchvision']
+    tv.datasets, tv.transforms, tv.models = (sys.modules['torchvision.datasets'], sys.modules['torchvision.transforms'],
+                                             sys.modules['torchvision.models'])
+    for cls in (scipy.sparse.csr_matrix, scipy.sparse.csr_array):
+        if not hasattr(cls, 'A'):
+            cls.A = property(lambda m: m.toarray())
+    import functions.utils as U
+    return U
+
+
+def _a9a_like(rs, n, with_id):
+    """a9a-shaped rows: 123 binary columns, 14 ones per row; optionally column 0 replaced by a
+    unique row id in (0, 1] so a shuffled batch reveals its order."""
+    X = np.zeros((n, 123), np.float32)
+    cols = np.argsort(rs.rand(n, 123), axis=1)[:, :14]
+    np.put_along_axis(X, cols, 1.0, axis=1)
+    if with_id:
+        X[:, 0] = (np.arange(n) + 1) / n
+    X[:, 122] = 1.0                    # last column populated: train and test files parse to equal width
+    return X
+
+
+def run_prep():
+    """exp.py:60-99 on synthetic LIBSVM files through the reference's load_full_data."""
+    import shutil
+    import tempfile
+    from sklearn.datasets import dump_svmlight_file
+    U = _reference_utils()
+    rs = np.random.RandomState(77)
+    n, nt, N, alpha, D, k_par = 3000, 400, 5, 0.5, 256, 0.1
+    X = _a9a_like(rs, n, True)
+    Xt = _a9a_like(rs, nt, False)
+    w = rs.normal(size=123)
+    y = np.where(X @ w > np.quantile(X @ w, 0.7), 1.0, -1.0)       # a9a's {-1, +1} labels
+    yt = np.where(Xt @ w > np.quantile(X @ w, 0.7), 1.0, -1.0)
+    tmp = tempfile.mkdtemp()
+    cwd = os.getcwd()
+    try:
+        os.makedirs(os.path.join(tmp, 'FedAMW', 'datasets'))
+        os.makedirs(os.path.join(tmp, 'work'))
+        dump_svmlight_file(X, y, os.path.join(tmp, 'FedAMW', 'datasets', 'a9a'), zero_based=False)
+        dump_svmlight_file(Xt, yt, os.path.join(tmp, 'FedAMW', 'datasets', 'a9a.t'), zero_based=False)
+        os.chdir(os.path.join(tmp, 'work'))              # utils.py:37 reads '../FedAMW/datasets/'
+        torch.manual_seed(100)                            # exp.py:28-29
+        np.random.seed(100)
+        with contextlib.redirect_stdout(io.StringIO()):
+            trainloader, testloader, parts, d, C = U.load_full_data('a9a', N, alpha)
+        # exp.py:61-99 (restated: iter(loader).next() -> next(iter(loader)))
+        X_train, y_all = next(iter(trainloader))
+        X_test, y_test = next(iter(testloader))
+        phi_all, phi_test = T.feature_mapping(X_train.reshape(1, X_train.shape[0], X_train.shape[1]), X_test, k_par,
+                                              D, 'gaussian')
+        phi_all = phi_all.reshape(-1, D)
+        hete = 0
+        Cm = torch.matmul(phi_all.T, phi_all) / len(phi_all)
+        Xc, yc = [], []
+        for idx in parts:
+            Xc.append(phi_all[idx, :])
+            yc.append(y_all[idx])
+            Cj = torch.matmul(Xc[-1].T, Xc[-1]) / len(Xc[-1])
+            hete += len(Xc[-1]) / len(phi_all) * torch.norm(Cm - Cj)
+        val_idx, train_idx = [], []
+        for i in range(N):
+            r = np.arange(Xc[i].shape[0])
+            np.random.shuffle(r)
+            cut = int(Xc[i].shape[0] * 0.2)
+            val_idx.append(r[:cut])
+            train_idx.append(r[cut:])
+        after_torch = torch.empty(4, dtype=torch.int64).random_().numpy()
+        after_np = np.random.randint(0, 1 << 30, 4)
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+    order = np.rint(X_train[:, 0].numpy() * n).astype(np.int64) - 1   # the full-batch pass's row order
+    cat = lambda a: np.concatenate([np.asarray(v, dtype=np.int64) for v in a])
+    lens = lambda a: np.array([len(v) for v in a], dtype=np.int64)
+    rec = dict(X=X, y=y, X_test=Xt, y_test=yt, n_clients=N, alpha=alpha, D=D, k_par=k_par, d=d, C=C,
+               parts=cat(parts), part_len=lens(parts), order=order, y_all=y_all.numpy(), y_test_out=y_test.numpy(),
+               val_idx=cat(val_idx), train_idx=cat(train_idx), split_len=lens(val_idx),
+               phi_head=np.stack([x[:4].numpy() for x in Xc]), phi_test_head=phi_test[:16].numpy(),
+               phi_sum=np.array([float(x.double().sum()) for x in Xc]), hete=np.float64(hete.item()),
+               after_torch=after_torch, after_np=after_np)
+    np.savez_compressed(os.path.join(OUT, 'prep_a9a.npz'), **rec)
+    print('prep_a9a parts', lens(parts), 'hete', float(hete))
+    # the partitioner alone at exp.py's setting (alpha = 0.01) on full-size label vectors
+    for name, labels, nc in (('a9a', (rs.rand(32561) < 0.24).astype(np.float64), 10),
+                             ('covtype', rs.choice(7, size=58101, p=[.36, .49, .06, .005, .016, .03, .039])
+                              .astype(np.float64), 50)):
+        np.random.seed(100)
+        with contextlib.redirect_stdout(io.StringIO()):
+            pr, counts = U.get_Dirichlet_distribution(labels, [1.0 / nc] * nc, 0.01)
+        np.savez_compressed(os.path.join(OUT, 'prep_dirichlet_%s.npz' % name), labels=labels.astype(np.int8),
+                            n_clients=nc, alpha=0.01, parts=cat(pr), part_len=lens(pr),
+                            after_np=np.random.randint(0, 1 << 30, 4))
+        print('dirichlet', name, lens(pr)[:10])
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params']
+    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params', 'long', 'prep']
+    if 'long' in which:
+        run_long()
+    if 'prep' in which:
+        run_prep()
     if 'rounds' in which:
         run_units()
         for case in CASES:

@@ -78,6 +78,45 @@ def test_prepare_matches_oracle(amd):
     assert abs(d['heterogeneity'] - r['hete']) <= 1e-4 * abs(r['hete'])
 
 
+def test_prepare_matches_reference_fixture(amd, tmp_path):
+    """experiment.prepare (LIBSVM parse, Dirichlet partition, full-batch replay, fs_feature_map,
+    fs_gram / fs_hetero, 20/80 split) on the LIBSVM files the reference's own load_full_data
+    read in make_golden.py (prep_a9a.npz), against the reference's outputs."""
+    from sklearn.datasets import dump_svmlight_file
+    from tests.fixtures import load
+    d = load('prep_a9a')
+    root = tmp_path / 'datasets'
+    root.mkdir()
+    dump_svmlight_file(d['X'], d['y'], str(root / 'a9a'), zero_based=False)
+    dump_svmlight_file(d['X_test'], d['y_test'], str(root / 'a9a.t'), zero_based=False)
+    N, D = int(d['n_clients']), int(d['D'])
+    torch.manual_seed(100)
+    np.random.seed(100)
+    r = amd.experiment.prepare('a9a', D, N, float(d['alpha']), {'kernel_par': float(d['k_par']),
+                                                                 'kernel_type': 'gaussian'},
+                               str(root) + '/', verbose=False)
+    np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['after_torch'])
+    np.testing.assert_array_equal(np.random.randint(0, 1 << 30, 4), d['after_np'])
+    off = np.concatenate([[0], np.cumsum(d['part_len'])])
+    parts = [d['parts'][off[i]:off[i + 1]] for i in range(N)]
+    assert [list(p) for p in r['index_partitions']] == [list(p) for p in parts]
+    soff = np.concatenate([[0], np.cumsum(d['split_len'])])
+    toff = np.concatenate([[0], np.cumsum(d['part_len'] - d['split_len'])])
+    yv = np.concatenate([d['y_all'][p][d['val_idx'][soff[j]:soff[j + 1]]] for j, p in enumerate(parts)])
+    np.testing.assert_array_equal(r['y_val'].numpy(), yv)
+    for j, p in enumerate(parts):
+        np.testing.assert_array_equal(r['y_train'][j].numpy(), d['y_all'][p][d['train_idx'][toff[j]:toff[j + 1]]])
+    # features (fs_feature_map vs torch's CPU map): the validation rows of every client's block
+    Xv = r['X_val'].numpy()
+    for j in range(N):
+        vi = d['val_idx'][soff[j]:soff[j + 1]]
+        for k, row in enumerate(vi):
+            if row < 4:
+                assert np.abs(Xv[soff[j] + k] - d['phi_head'][j][row]).max() <= 1e-5, (j, row)
+    assert np.abs(r['X_test'][:16].cpu().numpy() - d['phi_test_head']).max() <= 1e-5
+    assert abs(r['heterogeneity'] - float(d['hete'])) <= 1e-4 * abs(float(d['hete']))
+
+
 def test_experiment_end_to_end(amd, tmp_path):
     out = amd.experiment.run('a9a', D=64, num_partitions=4, local_epoch=1, Round=3, n_repeats=1, alpha_Dirk=0.5,
                              data_dir='/nonexistent/', result_dir=str(tmp_path), synth=dict(n_train=700, n_test=120),

@@ -8,8 +8,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load, positional,
-                            split_clients)
+from tests.fixtures import (LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
+                            load_long, positional, split_clients)
 
 pytestmark = pytest.mark.gpu
 
@@ -62,6 +62,25 @@ def test_dropin_matches_reference_golden(amd, name):
     if 'p' in d:
         p = stats['p'].cpu().numpy()
         assert np.abs(p - d['p'][-1]).max() <= P_RTOL * np.abs(d['p']).max()
+
+
+@pytest.mark.parametrize('name', LONG_CASES)
+def test_dropin_long_horizon_golden(amd, name):
+    """20 rounds at D = 1024, C = 10 against the reference (FedProx / FedAMW, chained and
+    parallel clients): fp32 drift over many rounds stays inside the stated tolerances."""
+    d = load_long(name)
+    (tr, tl, ta), stats = run_dropin(amd, d)
+    W = stats['W_rounds'][d['snap']]
+    for k in range(len(d['snap'])):
+        err = np.abs(W[k] - d['W'][k]).max()
+        assert err <= W_RTOL * np.abs(d['W'][k]).max(), (name, int(d['snap'][k]), err)
+    np.testing.assert_allclose(tr.numpy(), d['train_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl.numpy(), d['test_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta.numpy() - d['test_acc']).max() <= acc_tol(d)
+    if 'p' in d:
+        assert np.abs(stats['p'].cpu().numpy() - d['p'][-1]).max() <= P_RTOL * np.abs(d['p']).max()
 
 
 def test_dropin_consumes_rng_like_reference(amd):

@@ -4,8 +4,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
-                            positional, split_clients)
+from tests.fixtures import (LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
+                            load_long, positional, split_clients)
 
 
 def run_oracle(d):
@@ -67,3 +67,19 @@ def test_lr_schedule_compounds():
         seq.append(lr)
     assert seq[0] == 0.5 and seq[49] == 0.5
     assert abs(seq[50] - 0.05) < 1e-15 and abs(seq[75] - 0.0005) < 1e-15 and abs(seq[99] - 0.0005) < 1e-15
+
+
+@pytest.mark.parametrize('name', LONG_CASES)
+def test_long_horizon_matches_reference(name):
+    """20 rounds at D = 1024, C = 10 (FedProx / FedAMW, chained and parallel): the fp32 drift of
+    the restatement over many rounds stays inside the stated tolerances."""
+    d = load_long(name)
+    tr, tl, ta, trace = run_oracle(d)
+    snap = d['snap']
+    for k, t in enumerate(snap):
+        assert np.abs(trace['W'][t] - d['W'][k]).max() <= W_RTOL * np.abs(d['W'][k]).max(), (name, t)
+    np.testing.assert_allclose(tr, d['train_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl, d['test_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)
+    if 'p' in d:
+        assert np.abs(trace['p'] - d['p']).max() <= P_RTOL * np.abs(d['p']).max()
