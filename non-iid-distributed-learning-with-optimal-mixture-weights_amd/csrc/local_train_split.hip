@@ -116,15 +116,23 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
 // (fixed q) then reads 64 contiguous bytes of each of 16 rows.
-template <int RT, int G, bool PROX>
+// SCHED: how the 8 waves share a step's hand-off and the next step's row loads.
+//   0  every wave publishes / polls its share of the values; waves 0-3 issue their next
+//      rows right after the hand-off, waves 4-7 after the softmax.
+//   1  waves 4-7 write their image slice and issue their next rows at once (so half the next
+//      step's bytes stream during the hand-off); waves 0-3 alone run the hand-off (their
+//      vmcnt queue holds no row loads while they poll) and issue their rows after the softmax.
+//   2  as 1, but waves 0-3 issue their rows right after the hand-off.
+template <int RT, int G, bool PROX, int SCHED>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   constexpr int NW = SP_WAVES;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
-  // exchanged values per thread: NR*C logits + 2 norms (G >= 8 requires NR*C + 2 <= 512)
-  constexpr int M = (G >= 8) ? 1 : (NZ + 2 + SP_THREADS - 1) / SP_THREADS;
+  constexpr int XT = SCHED ? SP_THREADS / 2 : SP_THREADS;       // threads running the hand-off
+  // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= XT)
+  constexpr int M = (G >= 8) ? 1 : (NZ + 2 + XT - 1) / XT;
   __shared__ float zpart[NW][NR][NC];
   __shared__ float gbuf[NR][NC];
   __shared__ float zsum[NR][NC];
@@ -346,8 +354,12 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
     if (lc_ok) fetch_rows();                                                         \
   }
 
-      {
-        // ---- hand-off, spread over the threads: thread t owns the values t + 512 m
+      const bool xw = SCHED == 0 || w < NW / 2;      // this wave runs the hand-off
+      if (!xw) {
+        SP_IMG_WRITE();
+        SP_NEXT();
+      } else {
+        // ---- hand-off, spread over the hand-off threads: thread t owns the values t + XT m
         // (the B x C real logits row-major, then the two norms).  Guideline 16, R2 form:
         // every value travels as one 8-byte {tag, value} granule written by ONE relaxed
         // agent-scope (sc1) store -- the data is its own flag; the partners' granules are
@@ -360,7 +372,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         unsigned long long pl[M][G];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const int idx = tid + SP_THREADS * m;
+          const int idx = tid + XT * m;
           float v = 0.f;
           if (idx < NV - 2) {
             const int r = idx / C, c = idx - r * C;
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         auto poll = [&]() {
 #pragma unroll
           for (int m = 0; m < M; ++m) {
-            const int idx = tid + SP_THREADS * m;
+            const int idx = tid + XT * m;
 #pragma unroll
             for (int h = 0; h < G; ++h)
               pl[m][h] = __hip_atomic_load(slot + (int64_t)h * X.SZ + (idx < NV ? idx : 0), __ATOMIC_RELAXED,
@@ -397,7 +409,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           for (int m = 0; m < M; ++m)
 #pragma unroll
             for (int h = 0; h < G; ++h)
-              ok &= (h == g) | (tid + SP_THREADS * m >= NV) | ((unsigned)(pl[m][h] >> 32) == tag32);
+              ok &= (h == g) | (tid + XT * m >= NV) | ((unsigned)(pl[m][h] >> 32) == tag32);
           if (__all(ok)) break;
           if (dead || ++spins > X.spin_limit) {
             if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -410,7 +422,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         // sum in slice order 0..G-1 (own partial at position g): identical bits in every partner
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const int idx = tid + SP_THREADS * m;
+          const int idx = tid + XT * m;
           if (idx < NV) {
             float v = 0.f;
 #pragma unroll
@@ -424,7 +436,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           }
         }
         SP_STAMP(4)
-        if (w < NW / 2) SP_NEXT();
+        if ((SCHED == 0 || SCHED == 2) && w < NW / 2) SP_NEXT();
       }
       SP_STAMP(5)
       lds_barrier();  // S2: summed logits and norms, the image
@@ -453,7 +465,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       cep = wave_sum(cep);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
-      if (w >= NW / 2) SP_NEXT();
+      if ((SCHED == 0 && w >= NW / 2) || (SCHED == 1 && w < NW / 2)) SP_NEXT();
       SP_STAMP(7)
       const float pn2 = nrm[0], wn2 = nrm[1];
       if (g == 0 && tid == 0 && e == E - 1) {
@@ -586,12 +598,30 @@ static unsigned split_spin_limit() {
   return s ? (unsigned)strtoul(s, nullptr, 10) : SP_SPIN_LIMIT;
 }
 
+template <int RT, int G, bool PROX, int SCHED>
+static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, SCHED>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
+}
+
+static int split_sched(int G) {
+  const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
+  if (s) return std::max(0, std::min(2, atoi(s)));
+  return G >= 16 ? 0 : 1;
+}
+
 template <int RT, int G, bool PROX>
 static void launch_split_p(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
+  const int sc = split_sched(G);
+  if constexpr (G >= 16) {
+    launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);       // hand-off values need all 512 threads
+  } else {
+    if (sc == 0) launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);
+    else if (sc == 1) launch_split_s<RT, G, PROX, 1>(P, X, grid, lds, st);
+    else launch_split_s<RT, G, PROX, 2>(P, X, grid, lds, st);
+  }
 }
 
 template <int RT, int G>

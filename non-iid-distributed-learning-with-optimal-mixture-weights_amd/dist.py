@@ -5,8 +5,13 @@ The reference simulates clients serially in one process and has no collectives
 inside a round, so they are sharded across ranks and the only exchange per round
 is ONE all-reduce (sum, fp32) of the per-rank partial aggregates
 sum_{j in rank} p_j W_j  (C x ld floats; 80 KB at C=10, D=2048) -- a latency-bound
-collective over xGMI.  FedAMW additionally all-gathers the clients' weights so every
-rank runs the identical, deterministic p-solve (no broadcast needed).
+collective over xGMI.  FedAMW additionally needs every client model applied to the pooled
+validation set (Z, tools.py:448): each rank computes the Z columns of ITS clients (the
+sharded Z-GEMM, fs_mix_z), the ranks all-gather Z once per round, and every rank runs the
+identical, deterministic p-solve on it (no broadcast); the learned p then weights the same
+partial aggregate + all-reduce as FedAvg.  The solver's client axis is rank-major
+("solver order"): rank r's clients occupy columns r*L .. r*L + n_r - 1 of every class
+segment, L = max_r n_r rounded up to 4, the rest are zero columns whose p stays 0.
 ``clients='sequential'`` (the reference's chained clients) cannot shard: every rank
 runs a full replica.
 
@@ -65,3 +70,31 @@ def allgather_rows(local, counts, group=None):
     bufs = [torch.empty_like(pad) for _ in range(ws)]
     tdist.all_gather(bufs, pad, group=group)
     return torch.cat([b[:int(c)] for b, c in zip(bufs, counts)], 0)
+
+
+def solver_layout(shards):
+    """Client axis of the sharded p-solve: returns (L, pos) with L the per-rank block width
+    (max shard size rounded up to 4, so every rank's Z block has the same 16-byte aligned
+    shape) and pos[j] = the solver column of global client j (rank-major)."""
+    L = (max(len(s) for s in shards) + 3) // 4 * 4
+    n = sum(len(s) for s in shards)
+    pos = np.empty(n, dtype=np.int64)
+    for r, s in enumerate(shards):
+        pos[np.asarray(s, dtype=np.int64)] = r * L + np.arange(len(s))
+    return L, pos
+
+
+def allgather_z(Z_local, C, out, group=None):
+    """Z_local [n_v, C*L] (this rank's clients, class-major: column c*L + i) -> out
+    [n_v, C*R*L] in solver order (column c*(R*L) + r*L + i), R = world size.  One all-gather
+    of the contiguous per-rank blocks, then one layout copy."""
+    nv, CL = Z_local.shape
+    L = CL // C
+    R = world()[1]
+    if R == 1:
+        out.copy_(Z_local)
+        return out
+    buf = torch.empty((R * nv, CL), dtype=Z_local.dtype, device=Z_local.device)    # rank blocks along dim 0
+    tdist.all_gather_into_tensor(buf, Z_local.contiguous(), group=group)
+    out.view(nv, C, R, L).copy_(buf.view(R, nv, C, L).permute(1, 2, 0, 3))
+    return out

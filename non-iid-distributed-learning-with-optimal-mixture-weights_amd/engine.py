@@ -137,14 +137,15 @@ class LocalTrainer:
     mode as persistent groups over the clients, in chained mode as one group walking the
     chain); 1 forces one workgroup per client."""
 
-    def __init__(self, feats, C, B, E, split=None, chained=False):
+    def __init__(self, feats, C, B, E, split=None, chained=False, rows=None):
         self.f = feats
         self.C, self.B, self.E = int(C), int(B), int(E)
         dev = feats.device
         N = len(feats.ns)
         self.N = N
         self.chained = bool(chained)
-        self.W_out = torch.empty(N, self.C, feats.ld, device=dev, dtype=torch.float32)
+        # rows > N: zero padding clients after the real ones (the sharded FedAMW Z block)
+        self.W_out = torch.zeros(max(N, int(rows or 0)), self.C, feats.ld, device=dev, dtype=torch.float32)
         self.loss = torch.zeros(N, device=dev, dtype=torch.float64)
         # pass p = j*E + e  ->  (n_j, offset)
         ns = feats.ns
@@ -311,6 +312,13 @@ class Mixture:
     def check_errors(self):
         """Raise if a multi-CU p-solve reported a timed-out exchange (synchronises)."""
         _check_ws_error(self.ws, 'fs_mix_solve')
+
+    def z_block(self, W_all, n, out):
+        """fs_mix_z of ``n`` client models (W_all [n, C, ld]) on the validation rows into
+        ``out`` [n_val, C * ldN(n)] -- one rank's block of the sharded Z-GEMM."""
+        _lib.check(_lib.lib().fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, int(n), self.C, self.nv,
+                                       _lib.ptr(out), _lib.stream_ptr()), 'fs_mix_z')
+        return out
 
     def prepare(self, seeds, slot=0, stream=None):
         """Enqueue one round's validation-pass shuffles (one seed per inner epoch)."""

@@ -135,7 +135,13 @@ class Federation:
         self.feats = engine.Features([torch.as_tensor(X_train[j]) for j in mine],
                                      [torch.as_tensor(y_train[j]) for j in mine], D, dev)
         ld = self.ld = self.feats.ld
-        self.trainer = engine.LocalTrainer(self.feats, C, B, E, chained=self.chained)
+        # sharded FedAMW: the p-solve's client axis is rank-major blocks of L columns (dist.py)
+        self.zshard = algo == 'fedamw' and self.sharded
+        if self.zshard:
+            self.L, self.pos = dist.solver_layout(self.shards)
+            self.pos_dev = torch.from_numpy(self.pos).to(dev)
+        self.trainer = engine.LocalTrainer(self.feats, C, B, E, chained=self.chained,
+                                           rows=self.L if self.zshard else None)
         self.evaluator = engine.Evaluator(X_test, y_test, D, C, dev, ld)
         self.W_g = torch.zeros(C, ld, device=dev, dtype=torch.float32)
         self.W_g[:, :D].copy_(W_init)
@@ -149,8 +155,18 @@ class Federation:
             Bv = int(validloader.batch_size)
             if not isinstance(validloader.sampler, torch.utils.data.RandomSampler):
                 raise NotImplementedError('validloader must shuffle (exp.py:99)')
-            self.mixture = engine.Mixture(Xv, yv, D, C, N, Bv, self.p_all, dev, ld)
-            self.agg = engine.Aggregator(N, C, ld, dev)
+            if self.zshard:
+                Ns = nranks * self.L
+                p0 = torch.zeros(Ns, dtype=torch.float32)
+                p0[torch.from_numpy(self.pos)] = self.p_all
+                self.mixture = engine.Mixture(Xv, yv, D, C, Ns, Bv, p0, dev, ld)
+                self.Z_local = torch.empty(self.mixture.nv, C * self.L, device=dev, dtype=torch.float32)
+                lo = self.rank * self.L
+                self.p_slice = lambda p: p[lo:lo + len(mine)]
+                self.agg = engine.Aggregator(len(mine), C, ld, dev)
+            else:
+                self.mixture = engine.Mixture(Xv, yv, D, C, N, Bv, self.p_all, dev, ld)
+                self.agg = engine.Aggregator(N, C, ld, dev)
             self.p_hist = torch.empty(R, N, dtype=torch.float32, device=dev)
         else:
             self.agg = engine.Aggregator(len(mine), C, ld, dev)
@@ -194,13 +210,20 @@ class Federation:
         self.plan.round(t, self.lr, P[0])
         if self.on_local_train:
             self.on_local_train[1]()
-        if self.mixture is not None:
+        if self.zshard:
+            # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
+            # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
+            self.p_hist[t].copy_(self.mixture.p[self.pos_dev])
+            self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local)
+            dist.allgather_z(self.Z_local, self.C, self.mixture.Z)
+            p = self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False)
+            self.agg.run(self.trainer.W_out, self.p_slice(p), self.W_g)
+            dist.allreduce_sum_(self.W_g)
+            self.plan.round(t, self.lr, P[2])
+        elif self.mixture is not None:
             self.p_hist[t].copy_(self.mixture.p)
-            W_all = self.trainer.W_out
-            if self.sharded:
-                W_all = dist.allgather_rows(W_all, [len(s) for s in self.shards])[self.inv]
-            p = self.mixture.solve(W_all, None, self.lr_p, slot=t % 2)
-            self.agg.run(W_all, p, self.W_g)
+            p = self.mixture.solve(self.trainer.W_out, None, self.lr_p, slot=t % 2)
+            self.agg.run(self.trainer.W_out, p, self.W_g)
             self.plan.round(t, self.lr, P[2])
         elif self.sharded:
             self.plan.round(t, self.lr, P[1])
@@ -240,7 +263,8 @@ class Federation:
             if self.W_hist is not None:
                 self.stats['W_rounds'] = self.W_hist[:R, :, :D].cpu().numpy()
             if self.mixture is not None:
-                self.stats['p'] = self.mixture.p.detach().clone()
+                p = self.mixture.p[self.pos_dev] if self.zshard else self.mixture.p
+                self.stats['p'] = p.detach().clone()
         return train_loss, test_loss, test_acc
 
 

@@ -82,3 +82,78 @@ def test_two_rank_aggregate_and_seed_partition():
         assert np.abs(agg - ref).max() <= 1e-6 * np.abs(ref).max()     # fp32 summation-order noise only
         np.testing.assert_array_equal(gathered, seeds)                 # shards reassemble the global order
     np.testing.assert_array_equal(out[0][0], out[1][0])               # identical global model on every rank
+
+
+def _z_worker(rank, world, port, out):
+    """Sharded FedAMW layout: each rank builds the Z block of ITS clients, all-gathers it into
+    solver order; the solver-order matrix must equal the global Z with the columns permuted
+    by solver_layout, and p mapped there and back must round-trip."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        rs = np.random.RandomState(3)
+        N, C, nv = 11, 3, 5
+        ns = rs.randint(10, 100, size=N)
+        Zg = rs.normal(size=(nv, C, N)).astype(np.float32)          # global client order
+        shards = dist.shard_lpt(dist.client_work(ns, 2, 32), world)
+        L, pos = dist.solver_layout(shards)
+        mine = shards[rank]
+        Zl = np.zeros((nv, C, L), np.float32)
+        Zl[:, :, :len(mine)] = Zg[:, :, mine]
+        out_t = torch.empty(nv, C * world * L)
+        dist.allgather_z(torch.from_numpy(Zl.reshape(nv, C * L)), C, out_t)
+        out[rank] = (out_t.numpy(), L, pos)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_two_rank_sharded_z_layout():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_z_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rs = np.random.RandomState(3)
+    N, C, nv = 11, 3, 5
+    rs.randint(10, 100, size=N)
+    Zg = rs.normal(size=(nv, C, N)).astype(np.float32)
+    Z0, L, pos = out[0]
+    np.testing.assert_array_equal(Z0, out[1][0])                     # every rank holds the same Z
+    Zs = Z0.reshape(nv, C, world * L)
+    np.testing.assert_array_equal(Zs[:, :, pos], Zg)                 # solver column pos[j] = client j
+    pad = np.setdiff1d(np.arange(world * L), pos)
+    assert (Zs[:, :, pad] == 0).all() and L % 4 == 0                  # padding clients are zero columns
+    p = np.arange(N, dtype=np.float32) + 1
+    ps = np.zeros(world * L, np.float32)
+    ps[pos] = p
+    np.testing.assert_array_equal(ps[pos], p)
+
+
+def _rank_check_worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import fedamw_amd  # noqa: F401
+        from fedamw_amd.functions import tools
+        X = [torch.zeros(5, 8)]
+        y = [torch.zeros(5, dtype=torch.int64)]
+        try:
+            tools.FedAvg(X, y, X[0], y[0], 'classification', 2, 8, 0.1, 1, 32, False, 0.0, False, 0.0, 1,
+                         clients='parallel', verbose=False)
+            out[rank] = 'no error'
+        except ValueError as e:
+            out[rank] = str(e)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_parallel_clients_need_one_per_rank():
+    """N < world size with clients='parallel' is a clear ValueError on every rank (not a
+    'bad sizes' failure deep in the planner)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank_check_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert 'at least one client per rank' in out[r], out[r]

@@ -95,12 +95,14 @@ def _one_round(amd, algo, N, n, D, C, nt, shape, prox, mu, n_val=0, sample=(0, 1
     loss = _np(fed.loss_hist[0])
     assert np.isfinite(loss).all()
     # sampled clients against the oracle: replay the round's RNG (init draw, then 2 draws per
-    # training pass in client-major order)
+    # training pass in client-major order); round = 1 puts t = 0 at the first decay
+    # boundary int(R / 2) = 0 (tools.py:43-61), so round 0 trains at lr / 10
+    lr0 = O.lr_schedule(0, lr, 1)
     for j in sample:
         torch.manual_seed(seed)
         O.mlp_init(D, C)
         torch.empty(2 * E * j, dtype=torch.int64).random_()
-        Wr, lref = O.train_client(_np(d['X_train'][j]), _np(d['y_train'][j]), W0, lr, E, B, prox, mu,
+        Wr, lref = O.train_client(_np(d['X_train'][j]), _np(d['y_train'][j]), W0, lr0, E, B, prox, mu,
                                   algo == 'fedamw', 1e-5)
         assert np.abs(W_all[j] - Wr).max() <= 2e-5 * max(1.0, np.abs(Wr).max()), (j, np.abs(W_all[j] - Wr).max())
         assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
