@@ -18,9 +18,18 @@ Extra objects on the JSON line:
   roofline      fs_local_train (the dominant kernel): algorithmic HBM bytes per launch
                 (4*E*sum(n_j)*D + 8*E*sum(n_j) + 8*N*C*D) / mean launch time
                 from HIP events on the launch stream, against 8 TB/s; `traffic` = PMC HBM
-                bytes per launch from profiles/ (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE) or null.
+                bytes per launch from profiles/traffic_local_train_<config>.json (rocprofv3
+                FETCH_SIZE*2 + WRITE_SIZE), used only when its `source_rev` equals the
+                revision of the kernel sources being run (_lib.source_revision()), else null.
   cpu_baseline  the CPU oracle (oracle/fedsim_oracle.py, numpy restatement of the
                 reference round) timed on this host on whole rounds of the same workload.
+  fedamw        (config 2, one GPU) the other half of config 2 -- "FedAvg vs optimal
+                mixture weights": FedAMW rounds on the same clients plus 128 validation
+                rows each (tools.py:413-463): ms per round, the p-solve's sequential steps/s
+                and its bytes/s against 8 TB/s (4*R*N*C*n_v bytes of Z per round), the Z-GEMM's
+                TFLOP/s against the fp32 MFMA peak (2*N*C*D*n_v flop per round).
+Config 5 is BASELINE's 1000 clients over all GPUs (strong scaling: 1000/N clients per GPU);
+the others keep their per-GPU share fixed (weak scaling).
 """
 import argparse
 import json
@@ -40,6 +49,7 @@ from fedamw_amd import data as fdata  # noqa: E402
 from fedamw_amd.functions import tools  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+MFMA_F32_PEAK_TFS = 157.3   # dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md
 
 # BASELINE.json configs that fit one GPU, per-GPU shapes; config 4 is config 2's
 # FedAvg shape at 1,250 clients x 64 rows per GPU (10,000 clients on 8 GPUs).
@@ -47,10 +57,11 @@ PRESETS = {
     2: dict(algo='fedavg', clients=100, rows=512, D=2048, C=10, test=10000, shape='a9a'),
     3: dict(algo='fedprox', clients=1000, rows=465, D=4096, C=7, test=50000, shape='covtype'),
     4: dict(algo='fedavg', clients=1250, rows=64, D=2048, C=10, test=10000, shape='a9a'),
-    # config 5 whole on one GPU: FedAMW (mixture-weight solve every round) over 1000 clients x
-    # (128 train + 32 validation rows), D = 16384 (the p-solve is replicated per GPU anyway)
+    # config 5: FedAMW (mixture-weight solve every round) over 1000 clients in TOTAL x (128 train
+    # + 32 validation rows), D = 16384 -- strong scaling: each of N GPUs trains 1000/N clients
     5: dict(algo='fedamw', clients=1000, rows=128, D=16384, C=10, test=10000, shape='a9a'),
 }
+STRONG = {5}
 
 
 def parse():
@@ -72,6 +83,8 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--host-shuffle', action='store_true', help='replay shuffles on host threads, not the GPU')
+    ap.add_argument('--no-fedamw-leg', action='store_true', help='skip the FedAMW object of the config-2 line')
+    ap.add_argument('--fedamw-rounds', type=int, default=2, help='timed FedAMW rounds of the config-2 leg')
     a = ap.parse_args()
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
@@ -115,12 +128,71 @@ def cpu_baseline(d, args, budget):
 
 
 def load_traffic(tag, kernel='local_train'):
-    """PMC HBM bytes per launch measured for exactly this workload (profiles/), else None."""
+    """PMC HBM bytes per launch measured for exactly this workload AND these kernel sources
+    (profiles/traffic_<kernel>_<tag>.json with a matching source_rev), else None."""
+    from fedamw_amd import _lib
     path = os.path.join(ROOT, 'profiles', 'traffic_%s_%s.json' % (kernel, tag))
-    if os.path.exists(path):
-        with open(path) as f:
-            return json.load(f)
-    return None
+    if not os.path.exists(path):
+        return None, 'no PMC capture for this workload'
+    with open(path) as f:
+        rec = json.load(f)
+    rev = _lib.source_revision()
+    if rec.get('source_rev') != rev:
+        return None, 'stale PMC capture (kernel sources %s, measured on %s)' % (rev, rec.get('source_rev'))
+    return rec, 'PMC %s' % rec.get('source', '')
+
+
+def pool_validation(d, ws, dev):
+    """Every rank's clients contribute their validation rows; the pooled set (exp.py:92-99)
+    is identical on every rank: one all-gather of the per-rank blocks (equal sizes)."""
+    Xv, yv = d['X_val'], d['y_val']
+    if ws == 1:
+        return Xv, yv
+    bx = torch.empty((ws * Xv.shape[0],) + tuple(Xv.shape[1:]), dtype=Xv.dtype, device=dev)
+    by = torch.empty(ws * yv.shape[0], dtype=yv.dtype, device=dev)
+    tdist.all_gather_into_tensor(bx, Xv.contiguous())
+    tdist.all_gather_into_tensor(by, yv.contiguous())
+    return bx, by
+
+
+def phase_ms(events, name):
+    v = [a.elapsed_time(b) for n, a, b in events if n == name]
+    return float(np.mean(v)) if v else None
+
+
+def fedamw_leg(d, args, dev, rounds, warmup=1):
+    """The FedAMW half of config 2 on the same clients (one GPU)."""
+    N, E, B, R = args.clients, 2, 32, args.rounds
+    vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(d['X_val'], d['y_val']), batch_size=16,
+                                     shuffle=True)
+    torch.manual_seed(100)
+    fed = tools.Federation('fedamw', d['X_train'], d['y_train'], d['X_test'], d['y_test'], vl, 'classification',
+                           args.C, args.D, 0.5, E, B, False, 0.0, True, 1e-5, max(R, warmup + rounds), 1e-3,
+                           'parallel', verbose=False)
+    for _ in range(warmup):
+        fed.round()
+    torch.cuda.synchronize()
+    fed.events = []
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        fed.round()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    fed.results()
+    nv = fed.mixture.nv
+    steps = R * ((nv + 15) // 16)
+    z_ms, solve_ms, train_ms = (phase_ms(fed.events, k) for k in ('z', 'solve', 'train'))
+    z_flop = 2.0 * N * args.C * args.D * nv
+    solve_bytes = 4.0 * R * N * args.C * nv
+    return {'ms_per_round': 1e3 * el / rounds, 'client_rounds_per_s': N * rounds / el,
+            'train_ms': train_ms, 'z_gemm_ms': z_ms, 'z_gemm_tflops': z_flop / (z_ms * 1e-3) / 1e12,
+            'z_gemm_frac_mfma_f32': z_flop / (z_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
+            'p_solve_ms': solve_ms, 'p_solve_steps': steps, 'p_solve_us_per_step': 1e3 * solve_ms / steps,
+            'p_solve_steps_per_s': steps / (solve_ms * 1e-3), 'p_solve_gbs': solve_bytes / (solve_ms * 1e-3) / 1e9,
+            'p_solve_frac_hbm': solve_bytes / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            'p_solver': {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global'}.get(
+                fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
+            'n_val': nv, 'inner_epochs': R, 'rounds_timed': rounds}
 
 
 def main():
@@ -132,13 +204,17 @@ def main():
     dev = torch.device('cuda', local)
     if ws > 1:
         tdist.init_process_group('nccl', device_id=dev)
-    N_loc = args.clients
+    strong = args.config in STRONG and not args.custom
+    N_loc = args.clients // ws if strong else args.clients
+    if N_loc < 1:
+        raise SystemExit('bench: fewer clients than GPUs')
     E, B = 2, 32
-    if args.algo == 'fedamw' and ws > 1:
-        raise SystemExit('bench: --algo fedamw pools one validation set; run it with --gpus 1')
-    # every rank synthesises the full job's clients' identities but keeps only its own rows
-    d = fdata.federated(N_loc, args.rows, args.D, args.C, args.test,
-                        n_val=(args.rows // 4 if args.algo == 'fedamw' else 0), shape=args.shape,
+    fedamw = args.algo == 'fedamw'
+    leg = (args.config == 2 and not args.custom and not fedamw and ws == 1 and not args.no_fedamw_leg)
+    n_val = 128 if leg else (args.rows // 4 if fedamw else 0)
+    # every rank synthesises its own clients (seed 1000 + rank); the pooled validation set of
+    # FedAMW is all-gathered so that every rank solves the same p
+    d = fdata.federated(N_loc, args.rows, args.D, args.C, args.test, n_val=n_val, shape=args.shape,
                         seed=1000 + rank, device=dev)
     # the job's client list: Federation shards clients by LPT; this rank's synthetic clients are
     # placed at the positions it will own, the other ranks' rows are never touched here.
@@ -152,30 +228,18 @@ def main():
     lr, mu = 0.5, (5e-4 if args.algo == 'fedprox' else 0.0)
     R = max(args.rounds, args.warmup + args.steps)
     vl = None
-    if args.algo == 'fedamw':
-        vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(d['X_val'], d['y_val']), batch_size=16,
-                                         shuffle=True)
+    if fedamw:
+        Xv, yv = pool_validation(d, ws, dev)
+        vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(Xv, yv), batch_size=16, shuffle=True)
     torch.manual_seed(100)
     fed = tools.Federation(args.algo, Xs, ys, d['X_test'], d['y_test'], vl, 'classification', args.C, args.D, lr,
-                           E, B, args.algo == 'fedprox', mu, args.algo == 'fedamw', 1e-5, R, 1e-3,
+                           E, B, args.algo == 'fedprox', mu, fedamw, 1e-5, R, 1e-3,
                            'parallel', verbose=False, shuffle_device=not args.host_shuffle)
     assert len(fed.mine) == N_loc
-    ev_pairs = []
-
-    def before():
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        ev_pairs.append([e, None])
-
-    def after():
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        ev_pairs[-1][1] = e
-
     for _ in range(args.warmup):
         fed.round()
     torch.cuda.synchronize()
-    fed.on_local_train = (before, after)
+    fed.events = []
     if ws > 1:
         tdist.barrier()
     torch.cuda.synchronize()
@@ -190,38 +254,46 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         el = float(t.item())
-    lt_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_pairs]))
+    lt_ms = phase_ms(fed.events, 'train')
     tr, tl, ta = fed.results()
     n_rows = int(fed.feats.rows)
     alg_bytes = 4.0 * E * n_rows * args.D + 8.0 * E * n_rows + 8.0 * N_loc * args.C * args.D
     achieved = alg_bytes / (lt_ms * 1e-3) / 1e9
     tag = 'c%d%s' % (args.config, '' if args.algo == PRESETS[args.config]['algo'] else '_' + args.algo)
-    traffic = None if args.custom else load_traffic(tag)
+    traffic, tnote = (None, 'custom workload') if args.custom else load_traffic(tag)
+    total = N_loc * ws
     out = {
         'metric': 'client-rounds/sec (whole node)',
-        'value': N_loc * ws * args.steps / el,
+        'value': total * args.steps / el,
         'unit': 'client-rounds/s',
         'n_gpus': ws,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': 1e3 * el / args.steps,
         'higher_is_better': True,
-        'scaling': 'weak',
+        'scaling': 'strong' if strong else 'weak',
         'vs_baseline': None,
         'dtype': 'f32',
         'data': 'synthetic (%s-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)' % args.shape,
-        'config': {'workload': '%s: %s, %d clients/GPU x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
+        'config': {'workload': '%s: %s, %d clients%s x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
                                'round=%d, parallel clients'
-                               % ('custom' if args.custom else 'config %d' % args.config, args.algo, N_loc, args.rows,
-                                  args.D, args.C, E, B, args.test, R),
-                   'algo': args.algo, 'clients_total': N_loc * ws, 'rows_per_client': args.rows, 'D': args.D,
-                   'C': args.C, 'epochs': E, 'batch': B, 'test_rows': args.test, 'parallelism': 'clients%d' % ws},
+                               % ('custom' if args.custom else 'config %d' % args.config, args.algo, total,
+                                  '' if strong or ws == 1 else ' (%d/GPU)' % N_loc, args.rows, args.D, args.C, E, B,
+                                  args.test, R),
+                   'algo': args.algo, 'clients_total': total, 'clients_per_gpu': N_loc, 'rows_per_client': args.rows,
+                   'D': args.D, 'C': args.C, 'epochs': E, 'batch': B, 'test_rows': args.test,
+                   'parallelism': 'clients%d' % ws},
         'roofline': {'kernel': 'fs_local_train', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                     'traffic': (traffic or {}).get('bytes_per_launch'),
-                     'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes},
+                     'traffic': (traffic or {}).get('bytes_per_launch'), 'traffic_note': tnote,
+                     'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes, 'group_width': fed.trainer.G},
         'final_test_acc': float(ta[fed.t - 1]),
     }
+    if fedamw:
+        out['fedamw'] = {'z_gemm_ms': phase_ms(fed.events, 'z'), 'z_allgather_ms': phase_ms(fed.events, 'z_allgather'),
+                         'p_solve_ms': phase_ms(fed.events, 'solve'), 'n_val': fed.mixture.nv}
+    if leg:
+        out['fedamw'] = fedamw_leg(d, args, dev, args.fedamw_rounds)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(d, args, args.cpu_seconds)
     if rank == 0:

@@ -92,11 +92,13 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              the clients (LPT order, snake over the groups); chained clients: one
  *              group walks the chain with the weights kept in registers.  The error
  *              word (last 256 bytes of d_ws) is nonzero after the kernel if a partner
- *              never arrived (results invalid).
+ *              never arrived (results invalid).  fs_local_train_plan: *G_out on entry is
+ *              a request (0 = planner's choice, 1 = one workgroup per client, 2..16 = that
+ *              width if the shape allows it); prox says whether the FedProx term is on.
  * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
  * ------------------------------------------------------------------------- */
-int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int* G_out,
-                        int64_t* ws_bytes_out);
+int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
+                        int* G_out, int64_t* ws_bytes_out);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                    const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
                    float lr, float mu, int prox, float lam, int reg, int chained,

@@ -20,7 +20,7 @@ _SIGS = {
     'fs_randperm_device': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                      C.c_void_p]),
     'fs_local_train_plan': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int,
-                                      C.c_void_p, C.c_void_p]),
+                                      C.c_int, C.c_void_p, C.c_void_p]),
     'fs_local_train': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
                                  C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -116,3 +116,21 @@ def ptr(t):
 def stream_ptr(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return C.c_void_p(s.cuda_stream)
+
+
+def source_revision():
+    """sha256 (16 hex digits) of every kernel / C-ABI source of libfedsim.so (csrc/ and
+    include/fedsim.h).  Profiles under profiles/ record it; bench.py uses a PMC traffic
+    figure only when it was measured on kernels with this exact revision."""
+    import hashlib
+    import glob
+    pkg = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(pkg, 'csrc', '*.hip')) + glob.glob(os.path.join(pkg, 'csrc', '*.h'))
+                   + glob.glob(os.path.join(pkg, 'csrc', '*.cpp')))
+    files.append(os.path.join(os.path.dirname(pkg), 'include', 'fedsim.h'))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]

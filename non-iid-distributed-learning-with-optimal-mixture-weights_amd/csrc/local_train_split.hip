@@ -676,8 +676,9 @@ using namespace fs;
 // workspace bytes it needs.  On entry *G_out is a request: 0 = let the planner choose,
 // 1 = one workgroup per client, 2..16 = that group width if the shape allows it (else the
 // planner's choice).  FS_SPLIT_G in the environment overrides a 0 request (diagnostics).
+// prox: the FedProx term is on (its split variants carry the anchor in registers).
 // max_en = max_j E * n_j.
-extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained,
+extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                                    int* G_out, int64_t* ws_bytes_out) {
   FS_REQUIRE(G_out && ws_bytes_out, "null pointer");
   FS_REQUIRE(N >= 1 && B >= 1 && ld >= 64 && ld % 64 == 0, "bad sizes");
@@ -700,9 +701,13 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
           if (bytes / cand <= 32 * 1024) break;
         }
     } else {
-      // parallel clients: the narrowest group that fits (most clients in flight, fewest partners)
+      // parallel clients: the narrowest group that fits (most clients in flight, fewest partners).
+      // The prox variants hold the anchor slice in registers too and spill at 256 VGPRs; with
+      // enough clients to fill the chip one workgroup per client is as fast, so they split
+      // only when that leaves most CUs idle.
       for (int cand : {2, 4, 8, 16})
         if (split_fits(C, B, NT, cand) && cand <= cus) { G = cand; break; }
+      if (prox && G > 0 && 2 * N >= cus) G = 0;
     }
   }
   (void)max_en;

@@ -137,7 +137,7 @@ class LocalTrainer:
     mode as persistent groups over the clients, in chained mode as one group walking the
     chain); 1 forces one workgroup per client."""
 
-    def __init__(self, feats, C, B, E, split=None, chained=False, rows=None):
+    def __init__(self, feats, C, B, E, split=None, chained=False, rows=None, prox=False):
         self.f = feats
         self.C, self.B, self.E = int(C), int(B), int(E)
         dev = feats.device
@@ -160,7 +160,8 @@ class LocalTrainer:
         g, wsb = ctypes.c_int(0 if split is None else int(split)), ctypes.c_int64(0)
         max_en = int(self.E * ns.max()) if N else 0
         _lib.check(_lib.lib().fs_local_train_plan(N, self.C, self.B, self.E, feats.ld, max_en, int(self.chained),
-                                                  ctypes.byref(g), ctypes.byref(wsb)), 'fs_local_train_plan')
+                                                  int(bool(prox)), ctypes.byref(g), ctypes.byref(wsb)),
+                   'fs_local_train_plan')
         if split is not None and int(split) != g.value:
             raise _lib.FedsimError('fs_local_train_plan: G=%d is not available for this shape (planner: %d)'
                                    % (int(split), g.value))

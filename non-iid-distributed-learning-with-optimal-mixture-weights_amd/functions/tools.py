@@ -141,7 +141,7 @@ class Federation:
             self.L, self.pos = dist.solver_layout(self.shards)
             self.pos_dev = torch.from_numpy(self.pos).to(dev)
         self.trainer = engine.LocalTrainer(self.feats, C, B, E, chained=self.chained,
-                                           rows=self.L if self.zshard else None)
+                                           rows=self.L if self.zshard else None, prox=prox)
         self.evaluator = engine.Evaluator(X_test, y_test, D, C, dev, ld)
         self.W_g = torch.zeros(C, ld, device=dev, dtype=torch.float32)
         self.W_g[:, :D].copy_(W_init)
@@ -183,7 +183,7 @@ class Federation:
                                      reg=lambda_reg_if, lam=lambda_reg, chained=self.chained,
                                      shuffle_device=shuffle_device)
         self.t = 0
-        self.on_local_train = None      # optional (before, after) hooks around the local-training launch
+        self.events = None              # a list: round() appends (phase, start, end) HIP timing events
 
     def _prepare(self, t):
         """Draw round t's shuffle seeds (torch's global CPU generator, in the reference's
@@ -205,24 +205,33 @@ class Federation:
             self._prepare(0)
         self.lr = update_learning_rate(t, self.lr, self.R)
         P = _lib.PHASE_TRAIN, _lib.PHASE_AGGREGATE, _lib.PHASE_EVAL
-        if self.on_local_train:
-            self.on_local_train[0]()
-        self.plan.round(t, self.lr, P[0])
-        if self.on_local_train:
-            self.on_local_train[1]()
+        ev = self.events
+
+        def timed(name, fn):
+            if ev is None:
+                return fn()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            out = fn()
+            b.record()
+            ev.append((name, a, b))
+            return out
+
+        timed('train', lambda: self.plan.round(t, self.lr, P[0]))
         if self.zshard:
             # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
             self.p_hist[t].copy_(self.mixture.p[self.pos_dev])
-            self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local)
-            dist.allgather_z(self.Z_local, self.C, self.mixture.Z)
-            p = self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False)
+            timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local))
+            timed('z_allgather', lambda: dist.allgather_z(self.Z_local, self.C, self.mixture.Z))
+            p = timed('solve', lambda: self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False))
             self.agg.run(self.trainer.W_out, self.p_slice(p), self.W_g)
             dist.allreduce_sum_(self.W_g)
             self.plan.round(t, self.lr, P[2])
         elif self.mixture is not None:
             self.p_hist[t].copy_(self.mixture.p)
-            p = self.mixture.solve(self.trainer.W_out, None, self.lr_p, slot=t % 2)
+            timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.N, self.mixture.Z))
+            p = timed('solve', lambda: self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False))
             self.agg.run(self.trainer.W_out, p, self.W_g)
             self.plan.round(t, self.lr, P[2])
         elif self.sharded:
@@ -344,7 +353,7 @@ def _chain_train(X_train, y_train, W_init, D, C, lr, epoch, batch_size, prox, mu
     one fs_local_train launch in chained mode.  Consumes the generator like the reference
     (epoch passes per client, client-major).  Returns (feats, W_out [N, C, ld], loss [N])."""
     feats = engine.Features([torch.as_tensor(x) for x in X_train], [torch.as_tensor(y) for y in y_train], D, dev)
-    trainer = engine.LocalTrainer(feats, C, batch_size, epoch, chained=True)
+    trainer = engine.LocalTrainer(feats, C, batch_size, epoch, chained=True, prox=prox)
     trainer.upload_perms(rng.draw_pass_seeds(trainer.N * epoch))
     W0 = torch.zeros(C, feats.ld, device=dev, dtype=torch.float32)
     W0[:, :D].copy_(W_init)

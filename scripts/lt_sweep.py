@@ -48,7 +48,7 @@ def main():
     steps = int(np.sum(E * ((feats.ns + B - 1) // B)))
     for G in [int(g) for g in a.G.split(',')]:
         try:
-            tr = engine.LocalTrainer(feats, C, B, E, split=(G or None), chained=chained)
+            tr = engine.LocalTrainer(feats, C, B, E, split=(G or None), chained=chained, prox=a.prox)
         except fedamw_amd._lib.FedsimError as ex:
             print('config %d G=%d: n/a (%s)' % (a.config, G, ex), flush=True)
             continue

@@ -36,7 +36,7 @@ def test_abi_version():
                                 None, None, None, 1, None, 0, None), 'num_classes'),
     (lambda L: L.fs_local_train(None, 100, None, None, None, None, 1, 10, 32, 2, 0.1, 0.0, 0, 0.0, 0, 0,
                                 None, None, None, 1, None, 0, None), 'ld'),
-    (lambda L: L.fs_local_train_plan(0, 10, 32, 2, 64, 64, 0, None, None), 'null'),
+    (lambda L: L.fs_local_train_plan(0, 10, 32, 2, 64, 64, 0, 0, None, None), 'null'),
     (lambda L: L.fs_aggregate(None, 64, None, 0, 64, None, None, 0, 1, None), 'N'),
     (lambda L: L.fs_eval(None, 64, None, 0, None, 10, None, None, None), 'n'),
     (lambda L: L.fs_mix_solve(None, None, None, 5, 3, 10, 1, 65, 0.1, 0.9, None, None, None, None, 0, None),
