@@ -123,6 +123,11 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 //      step's bytes stream during the hand-off); waves 0-3 alone run the hand-off (their
 //      vmcnt queue holds no row loads while they poll) and issue their rows after the softmax.
 //   2  as 1, but waves 0-3 issue their rows right after the hand-off.
+//   3  "image first": every wave owns its tiles' LDS image exclusively, so it writes this
+//      step's rows from its registers into the image at the very start of the step and runs
+//      the forward from the image; waves 4-7 then refill their registers with the next
+//      step's rows at once (a whole step of lead time), waves 0-3 run the hand-off (nothing
+//      of theirs queued ahead of the polls) and refill after the softmax.
 template <int RT, int G, bool PROX, int SCHED>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   constexpr int NW = SP_WAVES;
@@ -131,8 +136,10 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
   constexpr int XT = SCHED ? SP_THREADS / 2 : SP_THREADS;       // threads running the hand-off
-  // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= XT)
-  constexpr int M = (G >= 8) ? 1 : (NZ + 2 + XT - 1) / XT;
+  // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
+  constexpr int M = (G >= 8) ? (SP_THREADS / XT) : (NZ + 2 + XT - 1) / XT;
+  // partners polled per round trip (bounded register use at large G)
+  constexpr int HC = (SCHED == 3 && G >= 8) ? 4 : G;
   __shared__ float zpart[NW][NR][NC];
   __shared__ float gbuf[NR][NC];
   __shared__ float zsum[NR][NC];
@@ -314,28 +321,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) lab[par][rt * 16 + l16] = lb[rt];
 
-      // ---------------- forward partial: z_g = X_slice W_slice^T (registers only) ----------------
-      floatx4 acc[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < TPW; ++i)
-        if (w + NW * i < NTS)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
-#pragma unroll
-              for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xf[i][rt][q], e4), comp(wr[i][q], e4), acc[rt]);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
-      SP_STAMP(1)
-      lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
-      SP_STAMP(2)
-
-      // image write: the backward of this step reads the slice from LDS
+      // image write: the backward of this step reads the slice from LDS (each wave only ever
+      // touches the image of its own tiles)
 #define SP_IMG_WRITE()                                                               \
   {                                                                                  \
     _Pragma("unroll") for (int i = 0; i < TPW; ++i)                                  \
@@ -344,20 +331,50 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           _Pragma("unroll") for (int q = 0; q < 4; ++q)                              \
             st4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg), xf[i][rt][q]); \
   }
-      // the next step's slice into the (now free) registers, then the row indices after it.
-      // Half of the waves issue those loads right after the hand-off, half after the
-      // softmax, so one wave of each SIMD computes while its partner is held up issuing loads.
+      // the next step's slice into the (now free) registers, then the row indices after it
 #define SP_NEXT()                                                                    \
   if (lc_ok) {                                                                       \
     SP_XLOAD();                                                                      \
     lc_ok = sp_advance(lc, P, grp, ng, T);                                           \
     if (lc_ok) fetch_rows();                                                         \
   }
+      if (SCHED == 3) {
+        SP_IMG_WRITE();
+        if (w >= NW / 2) SP_NEXT();
+      }
+
+      // ---------------- forward partial: z_g = X_slice W_slice^T ----------------
+      floatx4 acc[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+        if (w + NW * i < NTS)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 xa[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+              xa[rt] = SCHED == 3 ? ld4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg)) : xf[i][rt][q];
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4)
+#pragma unroll
+              for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xa[rt], e4), comp(wr[i][q], e4), acc[rt]);
+          }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
+      SP_STAMP(1)
+      lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
+      SP_STAMP(2)
 
       const bool xw = SCHED == 0 || w < NW / 2;      // this wave runs the hand-off
       if (!xw) {
-        SP_IMG_WRITE();
-        SP_NEXT();
+        if (SCHED != 3) {
+          SP_IMG_WRITE();
+          SP_NEXT();
+        }
       } else {
         // ---- hand-off, spread over the hand-off threads: thread t owns the values t + XT m
         // (the B x C real logits row-major, then the two norms).  Guideline 16, R2 form:
@@ -368,8 +385,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         // check, so the round trip neither queues behind nor waits for them.
         unsigned long long* slot = xb + ((int64_t)par * G) * X.SZ;
         const unsigned long long tag = (unsigned long long)tag32 << 32;
-        float own[M];
-        unsigned long long pl[M][G];
+        float own[M], sum[M];
+        unsigned long long pl[M][HC];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const int idx = tid + XT * m;
@@ -383,55 +400,62 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
             for (int i = 0; i < NW; ++i) v += wred[i][idx - (NV - 2)];
           }
           own[m] = v;
+          sum[m] = 0.f;
           if (idx < NV)
             __hip_atomic_store(slot + (int64_t)g * X.SZ + idx, tag | __float_as_uint(v), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         SP_STAMP(3)
-        auto poll = [&]() {
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const int idx = tid + XT * m;
-#pragma unroll
-            for (int h = 0; h < G; ++h)
-              pl[m][h] = __hip_atomic_load(slot + (int64_t)h * X.SZ + (idx < NV ? idx : 0), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-          }
-        };
-        poll();
-        SP_IMG_WRITE();
         if (X.spin_limit == 0 && gs == 0 && lane == 0)      // test knob: report an injected timeout
           __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
-        for (;;) {
-          bool ok = true;
+        // partners in chunks of HC (one round trip each); the sum runs in slice order
+        // 0..G-1 with the own partial at position g: identical bits in every partner
+#pragma unroll
+        for (int h0 = 0; h0 < G; h0 += HC) {
+          auto poll = [&]() {
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              const int idx = tid + XT * m;
+#pragma unroll
+              for (int h = 0; h < HC; ++h)
+                pl[m][h] = __hip_atomic_load(slot + (int64_t)(h0 + h) * X.SZ + (idx < NV ? idx : 0),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          };
+          poll();
+          if (SCHED != 3 && h0 == 0) SP_IMG_WRITE();
+          for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+              for (int h = 0; h < HC; ++h)
+                ok &= (h0 + h == g) | (tid + XT * m >= NV) | ((unsigned)(pl[m][h] >> 32) == tag32);
+            if (__all(ok)) break;
+            if (dead || ++spins > X.spin_limit) {
+              if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              dead = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            poll();
+          }
 #pragma unroll
           for (int m = 0; m < M; ++m)
 #pragma unroll
-            for (int h = 0; h < G; ++h)
-              ok &= (h == g) | (tid + XT * m >= NV) | ((unsigned)(pl[m][h] >> 32) == tag32);
-          if (__all(ok)) break;
-          if (dead || ++spins > X.spin_limit) {
-            if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            dead = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          poll();
+            for (int h = 0; h < HC; ++h)
+              sum[m] += (h0 + h == g) ? own[m] : __uint_as_float((unsigned)pl[m][h]);
         }
-        // sum in slice order 0..G-1 (own partial at position g): identical bits in every partner
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const int idx = tid + XT * m;
           if (idx < NV) {
-            float v = 0.f;
-#pragma unroll
-            for (int h = 0; h < G; ++h) v += (h == g) ? own[m] : __uint_as_float((unsigned)pl[m][h]);
             if (idx < NV - 2) {
               const int r = idx / C, c = idx - r * C;
-              zsum[r][c] = v;
+              zsum[r][c] = sum[m];
             } else {
-              nrm[idx - (NV - 2)] = v;            // ||W - W_a||^2, ||W||^2 at the start of this step
+              nrm[idx - (NV - 2)] = sum[m];       // ||W - W_a||^2, ||W||^2 at the start of this step
             }
           }
         }
@@ -465,7 +489,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       cep = wave_sum(cep);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
-      if ((SCHED == 0 && w >= NW / 2) || (SCHED == 1 && w < NW / 2)) SP_NEXT();
+      if ((SCHED == 0 && w >= NW / 2) || ((SCHED == 1 || SCHED == 3) && w < NW / 2)) SP_NEXT();
       SP_STAMP(7)
       const float pn2 = nrm[0], wn2 = nrm[1];
       if (g == 0 && tid == 0 && e == E - 1) {
@@ -608,7 +632,7 @@ static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t
 
 static int split_sched(int G) {
   const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
-  if (s) return std::max(0, std::min(2, atoi(s)));
+  if (s) return std::max(0, std::min(3, atoi(s)));
   return G >= 16 ? 0 : 1;
 }
 
@@ -616,11 +640,13 @@ template <int RT, int G, bool PROX>
 static void launch_split_p(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   const int sc = split_sched(G);
   if constexpr (G >= 16) {
-    launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);       // hand-off values need all 512 threads
+    if (sc == 3) launch_split_s<RT, G, PROX, 3>(P, X, grid, lds, st);
+    else launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);
   } else {
     if (sc == 0) launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);
     else if (sc == 1) launch_split_s<RT, G, PROX, 1>(P, X, grid, lds, st);
-    else launch_split_s<RT, G, PROX, 2>(P, X, grid, lds, st);
+    else if (sc == 2) launch_split_s<RT, G, PROX, 2>(P, X, grid, lds, st);
+    else launch_split_s<RT, G, PROX, 3>(P, X, grid, lds, st);
   }
 }
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 PMC passes (scripts/pmc_capture.sh) into profiles/.
 
-    python scripts/pmc_summary.py <tag> <kernel-substring> [round]
+    python scripts/pmc_summary.py <tag> <kernel-substring> [round [source_rev]]
 
 HBM traffic per launch of the named kernel, corrected as MI355X_MICROARCH.md's HBM section
 prescribes: gfx950 FETCH_SIZE counts exactly half the bytes of a wide coalesced (16 B/lane)
@@ -23,15 +23,17 @@ sys.path.insert(0, ROOT)
 def main():
     tag, kname = sys.argv[1], sys.argv[2]
     rnd = sys.argv[3] if len(sys.argv) > 3 else 'r02'
-    import fedamw_amd  # noqa: F401
-    from fedamw_amd import _lib
     src = os.path.join(ROOT, 'gpurun_out', 'pmc_' + tag)
     vals = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(src, 'p*', '**', '*counter_collection.csv'), recursive=True)):
         for r in csv.DictReader(open(f)):
             k = r['Kernel_Name'].split('(')[0].replace('void ', '')
             vals[(k, r['Counter_Name'])].append(float(r['Counter_Value']))
-    rev = _lib.source_revision()
+    # the kernel-source revision the passes ran on (written by pmc_capture.sh on the GPU box)
+    rev_file = os.path.join(src, 'source_rev.txt')
+    rev = open(rev_file).read().strip() if os.path.exists(rev_file) else (sys.argv[4] if len(sys.argv) > 4 else None)
+    if not rev:
+        raise SystemExit('no source_rev.txt in %s: pass the revision the capture ran on as argv[4]' % src)
     lines = ['# PMC summary %s (kernel sources %s); per-dispatch means' % (tag, rev)]
     for (k, c), v in sorted(vals.items()):
         lines.append('%-60s %-26s n=%-3d mean=%.6g' % (k[:60], c, len(v), sum(v) / len(v)))
