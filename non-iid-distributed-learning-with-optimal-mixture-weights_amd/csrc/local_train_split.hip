@@ -116,30 +116,27 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
 // (fixed q) then reads 64 contiguous bytes of each of 16 rows.
-// SCHED: how the 8 waves share a step's hand-off and the next step's row loads.
-//   0  every wave publishes / polls its share of the values; waves 0-3 issue their next
-//      rows right after the hand-off, waves 4-7 after the softmax.
-//   1  waves 4-7 write their image slice and issue their next rows at once (so half the next
-//      step's bytes stream during the hand-off); waves 0-3 alone run the hand-off (their
-//      vmcnt queue holds no row loads while they poll) and issue their rows after the softmax.
-//   2  as 1, but waves 0-3 issue their rows right after the hand-off.
-//   3  "image first": every wave owns its tiles' LDS image exclusively, so it writes this
-//      step's rows from its registers into the image at the very start of the step and runs
-//      the forward from the image; waves 4-7 then refill their registers with the next
-//      step's rows at once (a whole step of lead time), waves 0-3 run the hand-off (nothing
-//      of theirs queued ahead of the polls) and refill after the softmax.
-template <int RT, int G, bool PROX, int SCHED>
-__global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
-  constexpr int NW = SP_WAVES;
+// NWV: waves per workgroup -- 8 (one workgroup per CU, up to 16 tiles per slice) or 4 (two
+//      workgroups per CU, up to 8 tiles each: two independent client chains share the CU, so
+//      one computes while the other waits on its hand-off or its row loads).
+// SCHED: how the waves share a step's hand-off and the next step's row loads.
+//   0  every wave publishes / polls its share of the values; the first half of the waves
+//      issue their next rows right after the hand-off, the second half after the softmax.
+//   1  the second half writes its image slice and issues its next rows at once (their bytes
+//      stream during the hand-off); the first half alone runs the hand-off (nothing of its
+//      own queued ahead of its polls) and issues its rows after the softmax.
+template <int RT, int G, bool PROX, int SCHED, int NWV>
+__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_kernel(LTParams P, SplitWS X) {
+  constexpr int NW = NWV;
+  constexpr int NTH = NW * 64;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
-  constexpr int XT = SCHED ? SP_THREADS / 2 : SP_THREADS;       // threads running the hand-off
+  constexpr int XT = SCHED ? NTH / 2 : NTH;       // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
-  constexpr int M = (G >= 8) ? (SP_THREADS / XT) : (NZ + 2 + XT - 1) / XT;
-  // partners polled per round trip (bounded register use at large G)
-  constexpr int HC = (SCHED == 3 && G >= 8) ? 4 : G;
+  constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
+  constexpr int HC = G;                             // partners polled per round trip
   __shared__ float zpart[NW][NR][NC];
   __shared__ float gbuf[NR][NC];
   __shared__ float zsum[NR][NC];
@@ -338,10 +335,6 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
     lc_ok = sp_advance(lc, P, grp, ng, T);                                           \
     if (lc_ok) fetch_rows();                                                         \
   }
-      if (SCHED == 3) {
-        SP_IMG_WRITE();
-        if (w >= NW / 2) SP_NEXT();
-      }
 
       // ---------------- forward partial: z_g = X_slice W_slice^T ----------------
       floatx4 acc[RT];
@@ -355,7 +348,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
             float4 xa[RT];
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
-              xa[rt] = SCHED == 3 ? ld4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg)) : xf[i][rt][q];
+              xa[rt] = xf[i][rt][q];
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4)
 #pragma unroll
@@ -371,10 +364,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 
       const bool xw = SCHED == 0 || w < NW / 2;      // this wave runs the hand-off
       if (!xw) {
-        if (SCHED != 3) {
-          SP_IMG_WRITE();
-          SP_NEXT();
-        }
+        SP_IMG_WRITE();
+        SP_NEXT();
       } else {
         // ---- hand-off, spread over the hand-off threads: thread t owns the values t + XT m
         // (the B x C real logits row-major, then the two norms).  Guideline 16, R2 form:
@@ -424,7 +415,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
             }
           };
           poll();
-          if (SCHED != 3 && h0 == 0) SP_IMG_WRITE();
+          if (h0 == 0) SP_IMG_WRITE();
           for (;;) {
             bool ok = true;
 #pragma unroll
@@ -460,14 +451,14 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           }
         }
         SP_STAMP(4)
-        if ((SCHED == 0 || SCHED == 2) && w < NW / 2) SP_NEXT();
+        if (SCHED == 0 && w < NW / 2) SP_NEXT();
       }
       SP_STAMP(5)
       lds_barrier();  // S2: summed logits and norms, the image
       SP_STAMP(6)
       const float invb = 1.0f / (float)bc;
       float cep = 0.f;
-      for (int idx = tid; idx < NZ; idx += SP_THREADS) {   // NC lanes of one wave hold one row
+      for (int idx = tid; idx < NZ; idx += NTH) {          // NC lanes of one wave hold one row
         const int r = idx / NC, c = idx - r * NC;
         const bool valid = r < bc && c < C;
         const float z = valid ? zsum[r][c] : 0.f;
@@ -489,7 +480,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       cep = wave_sum(cep);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
-      if ((SCHED == 0 && w >= NW / 2) || ((SCHED == 1 || SCHED == 3) && w < NW / 2)) SP_NEXT();
+      if ((SCHED == 0 && w >= NW / 2) || (SCHED == 1 && w < NW / 2)) SP_NEXT();
       SP_STAMP(7)
       const float pn2 = nrm[0], wn2 = nrm[1];
       if (g == 0 && tid == 0 && e == E - 1) {
@@ -586,35 +577,47 @@ static size_t split_dyn_lds(int RT, int NT, int G) {
   return sizeof(float) * (size_t)(RT * 16) * (size_t)(tiles * 64 + 8);
 }
 
-static size_t split_static_lds(int RT) {
+static size_t split_static_lds(int RT, int NW) {
   const int NR = RT * 16;
-  return (size_t)SP_WAVES * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + SP_WAVES * 3 * 4 + 8 + 64;
+  return (size_t)NW * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + NW * 3 * 4 + 8 + 64;
 }
 
 static int split_rt(int B) { return B <= 16 ? 1 : 2; }
+
+// waves per workgroup implied by the slice width: 4 (two workgroups per CU) when the slice has
+// at most 8 tiles and two workgroups' LDS fit one CU, else 8 (FS_SPLIT_NW=8 forces 8)
+static int split_nw(int RT, int NT, int G) {
+  const int tiles = (NT + G - 1) / G;
+  const char* force = getenv("FS_SPLIT_NW");
+  if (force && atoi(force) == 8) return 8;
+  if (tiles <= 2 * 4 && 2 * (split_dyn_lds(RT, NT, G) + split_static_lds(RT, 4)) <= 160 * 1024) return 4;
+  return 8;
+}
 
 // can G workgroups split one client of this shape?
 static bool split_fits(int C, int B, int NT, int G) {
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
   if (C > 16 || B > 32 || NT < G) return false;
   const int RT = split_rt(B);
+  const int NW = split_nw(RT, NT, G);
   const int tiles = (NT + G - 1) / G;
-  if ((tiles + SP_WAVES - 1) / SP_WAVES > SP_TPW) return false;
-  if (G >= 8 && RT * 16 * C + 2 > SP_THREADS) return false;   // one exchanged value per thread
-  return split_dyn_lds(RT, NT, G) + split_static_lds(RT) <= 160 * 1024;
+  if ((tiles + NW - 1) / NW > SP_TPW) return false;
+  if (G >= 8 && RT * 16 * C + 2 > 512) return false;   // exchanged values: at most 512
+  return split_dyn_lds(RT, NT, G) + split_static_lds(RT, NW) <= 160 * 1024;
 }
 
 static int split_sz(int RT) { return RT * 16 * 16 + 4; }
 
-static int split_groups(int N, int G, int chained, int cus) {
-  return chained ? 1 : std::max(1, std::min(N, cus / G));
+// groups in flight: one per G workgroups, one workgroup per CU (8 waves) or two (4 waves)
+static int split_groups(int N, int G, int NW, int chained, int cus) {
+  return chained ? 1 : std::max(1, std::min(N, cus * (NW == 4 ? 2 : 1) / G));
 }
 
 static int64_t split_xbuf_bytes(int ngroups, int G, int RT) { return (int64_t)ngroups * 2 * G * split_sz(RT) * 8; }
 
-static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus) {
+static int64_t split_ws_bytes(int N, int G, int B, int NT, int chained, int cus) {
   const int RT = split_rt(B);
-  return split_xbuf_bytes(split_groups(N, G, chained, cus), G, RT) + SP_ERR_BYTES;
+  return split_xbuf_bytes(split_groups(N, G, split_nw(RT, NT, G), chained, cus), G, RT) + SP_ERR_BYTES;
 }
 
 static unsigned split_spin_limit() {
@@ -622,38 +625,40 @@ static unsigned split_spin_limit() {
   return s ? (unsigned)strtoul(s, nullptr, 10) : SP_SPIN_LIMIT;
 }
 
-template <int RT, int G, bool PROX, int SCHED>
+template <int RT, int G, bool PROX, int SCHED, int NW>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, SCHED>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, SCHED, NW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED, NW>), dim3(grid), dim3(NW * 64), lds, st, P, X);
 }
 
-static int split_sched(int G) {
+static int split_sched(int G, int NW) {
   const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
-  if (s) return std::max(0, std::min(3, atoi(s)));
-  return G >= 16 ? 0 : 1;
+  if (s) return std::max(0, std::min(1, atoi(s)));
+  return (G >= 16 || NW == 4) ? 0 : 1;           // (4-wave hand-off threads: all of them)
 }
 
 template <int RT, int G, bool PROX>
-static void launch_split_p(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  const int sc = split_sched(G);
+static void launch_split_p(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
+  const int sc = split_sched(G, NW);
   if constexpr (G >= 16) {
-    if (sc == 3) launch_split_s<RT, G, PROX, 3>(P, X, grid, lds, st);
-    else launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);
+    launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);     // the hand-off values need all 512 threads
   } else {
-    if (sc == 0) launch_split_s<RT, G, PROX, 0>(P, X, grid, lds, st);
-    else if (sc == 1) launch_split_s<RT, G, PROX, 1>(P, X, grid, lds, st);
-    else if (sc == 2) launch_split_s<RT, G, PROX, 2>(P, X, grid, lds, st);
-    else launch_split_s<RT, G, PROX, 3>(P, X, grid, lds, st);
+    if (NW == 4) {
+      if (sc == 0) launch_split_s<RT, G, PROX, 0, 4>(P, X, grid, lds, st);
+      else launch_split_s<RT, G, PROX, 1, 4>(P, X, grid, lds, st);
+    } else {
+      if (sc == 0) launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);
+      else launch_split_s<RT, G, PROX, 1, 8>(P, X, grid, lds, st);
+    }
   }
 }
 
 template <int RT, int G>
-static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (P.prox) launch_split_p<RT, G, true>(P, X, grid, lds, st);
-  else launch_split_p<RT, G, false>(P, X, grid, lds, st);
+static void launch_split_g(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
+  if (P.prox) launch_split_p<RT, G, true>(P, X, NW, grid, lds, st);
+  else launch_split_p<RT, G, false>(P, X, NW, grid, lds, st);
 }
 
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
@@ -666,7 +671,8 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
   if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");
-  const int ng = split_groups(P.N, G, P.chained, cus);
+  const int NW = split_nw(RT, NT, G);
+  const int ng = split_groups(P.N, G, NW, P.chained, cus);
   const int64_t xbytes = split_xbuf_bytes(ng, G, RT);
   if (!ws || ws_bytes < xbytes + SP_ERR_BYTES) return fail(FS_EINVAL, "fs_local_train: workspace too small");
   char* base = reinterpret_cast<char*>(ws);
@@ -686,7 +692,7 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   const size_t lds = split_dyn_lds(RT, NT, G);
   const int grid = P.chained ? 8 * G : ng * G;
 #define FS_SPLIT_CASE(rt, g) \
-  if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, grid, lds, st); return FS_OK; }
+  if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, NW, grid, lds, st); return FS_OK; }
   FS_SPLIT_CASE(2, 2) FS_SPLIT_CASE(2, 4) FS_SPLIT_CASE(2, 8) FS_SPLIT_CASE(2, 16)
   FS_SPLIT_CASE(1, 2) FS_SPLIT_CASE(1, 4) FS_SPLIT_CASE(1, 8) FS_SPLIT_CASE(1, 16)
 #undef FS_SPLIT_CASE
@@ -740,6 +746,6 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   (void)E;
   if (G == 0) return FS_OK;
   *G_out = G;
-  *ws_bytes_out = split_ws_bytes(N, G, B, chained, cus);
+  *ws_bytes_out = split_ws_bytes(N, G, B, NT, chained, cus);
   return FS_OK;
 }

@@ -169,10 +169,14 @@ def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, mode):
 @pytest.mark.parametrize('G', [2, 4, 8, 16])
 @pytest.mark.parametrize('chained', [True, False])
 @pytest.mark.parametrize('prox', [True, False])
-def test_local_train_split_widths(amd, G, chained, prox):
+@pytest.mark.parametrize('nw', [4, 8])
+def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
     """Every group width of the split-client kernel, chained (one group walks the chain) and
-    parallel, against the oracle: D = 1000 (16 tiles, the last one ragged), C = 10, tail
-    batches of 1 and 7 rows, and a client with no rows (its result is its start)."""
+    parallel, 4-wave (two workgroups per CU) and 8-wave workgroups, against the oracle:
+    D = 1000 (16 tiles, the last one ragged), C = 10, tail batches of 1 and 7 rows, and a
+    client with no rows (its result is its start)."""
+    if nw == 8:
+        monkeypatch.setenv('FS_SPLIT_NW', '8')
     rs = np.random.RandomState(G + 10 * chained + 100 * prox)
     D, C, B, E = 1000, 10, 32, 2
     sizes = [65, 33, 0, 7, 96, 40]
