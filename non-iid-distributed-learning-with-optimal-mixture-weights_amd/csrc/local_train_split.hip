@@ -585,11 +585,14 @@ static size_t split_static_lds(int RT, int NW) {
 static int split_rt(int B) { return B <= 16 ? 1 : 2; }
 
 // waves per workgroup implied by the slice width: 4 (two workgroups per CU) when the slice has
-// at most 8 tiles and two workgroups' LDS fit one CU, else 8 (FS_SPLIT_NW=8 forces 8)
+// at most 8 tiles and two workgroups' LDS fit one CU -- only on request (FS_SPLIT_NW=4): two
+// half-size chains per CU measured slower than one full one at every BASELINE shape (r02f:
+// config 2 462 vs 364 us, config 4 604 vs 497 us, chained config 1 11.4 vs 10.3 ms), since
+// the CU's memory pipe, not the chain's latency, is what both chains wait on
 static int split_nw(int RT, int NT, int G) {
   const int tiles = (NT + G - 1) / G;
   const char* force = getenv("FS_SPLIT_NW");
-  if (force && atoi(force) == 8) return 8;
+  if (!(force && atoi(force) == 4)) return 8;
   if (tiles <= 2 * 4 && 2 * (split_dyn_lds(RT, NT, G) + split_static_lds(RT, 4)) <= 160 * 1024) return 4;
   return 8;
 }

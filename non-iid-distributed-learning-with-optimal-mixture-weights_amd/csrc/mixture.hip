@@ -547,6 +547,260 @@ static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, cons
 }
 
 // ----------------------------------------------------------------------------
+// p-solve, register-resident form 2 (Bv <= 16, C <= CL <= 10, N <= 64*NK): the register
+// solver above is VALU-bound (rocprofv3: the SIMDs' vector pipes ~80 % busy at config 2);
+// this form does the same arithmetic in fewer vector instructions per step:
+//   * 8 waves x 2 batch rows (rows w and w + 8): the per-step fixed work -- the cross-wave
+//     gradient sum and the momentum step, which every wave repeats -- runs 8 times, not 16,
+//     and the two rows' reductions interleave (independent DPP chains, fewer wait states);
+//   * the batch's row indices and labels are wave-uniform: scalar loads, so the vector
+//     memory queue holds only Z rows and the ring of in-flight steps stays DEPTH deep;
+//   * Z rows through one buffer descriptor: row and class offsets are scalar (soffset), the
+//     lane's client offset the only vector address operand;
+//   * the two cross-half levels of the logits' reduce-scatter (lane distance 32 and 16) as
+//     one v_permlane{32,16}_swap of (a, b) plus one add: after the swap every lane holds its
+//     own and its partner's copy of the element it keeps (SWAP = 0 keeps the select form).
+// ----------------------------------------------------------------------------
+constexpr int M2_WAVES = 8;
+
+// reduce-scatter level at lane distance OFF over pairs (a, b): lanes with (lane & OFF) keep b
+template <int OFF, bool SWAP>
+__device__ __forceinline__ float rs_level(float a, float b, int lane) {
+  if constexpr (SWAP && (OFF == 32 || OFF == 16)) {
+    // inline asm, not the builtin: with a constant-zero partner (padding classes) hipcc
+    // 7.2 drops the builtin's second result and sums r0 + 0.  The pad inside the string is
+    // the 2 wait states a VALU write of either operand needs before v_permlane*_swap reads it.
+    if constexpr (OFF == 32)
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    else
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return a + b;
+  } else {
+    return rs_pair(a, b, OFF, lane);
+  }
+}
+
+// class_totals of lanes.h for two independent rows at once (the levels interleave)
+template <int CP, bool SWAP>
+__device__ __forceinline__ void class_totals2(float (&v0)[CP], float (&v1)[CP], int lane, float& o0, float& o1) {
+  constexpr int LPC = 64 / CP;
+#define M2_LEVEL(OFF_)                                                              \
+  if constexpr (CP >= 64 / (OFF_)) {                                               \
+    constexpr int L_ = CP / (32 / (OFF_));                                         \
+    _Pragma("unroll") for (int i = 0; i < L_ / 2; ++i) {                           \
+      v0[i] = rs_level<OFF_, SWAP>(v0[i], v0[i + L_ / 2], lane);                   \
+      v1[i] = rs_level<OFF_, SWAP>(v1[i], v1[i + L_ / 2], lane);                   \
+    }                                                                              \
+  }
+  M2_LEVEL(32) M2_LEVEL(16) M2_LEVEL(8) M2_LEVEL(4) M2_LEVEL(2) M2_LEVEL(1)
+#undef M2_LEVEL
+  float a = v0[0], b = v1[0];
+#pragma unroll
+  for (int off = LPC / 2; off >= 1; off >>= 1) {
+    a += xor_get(a, off, lane);
+    b += xor_get(b, off, lane);
+  }
+  o0 = a;
+  o1 = b;
+}
+
+template <int NK, int CP, int CL, int DEPTH, bool SWAP>
+__global__ __launch_bounds__(M2_WAVES * 64) void mix_solve_reg2_kernel(const float* __restrict__ Z,
+                                                                      const int32_t* __restrict__ y,
+                                                                      const int32_t* __restrict__ perms, int N, int C,
+                                                                      int nv, int epochs, int Bv, float lr, float mom,
+                                                                      float* __restrict__ p, float* __restrict__ buf,
+                                                                      int* __restrict__ first_flag, int z_bytes) {
+  static_assert(CL <= CP && CP <= 32 && (CP & (CP - 1)) == 0, "class padding");
+  static_assert(2 * CL * DEPTH <= 63, "ring vs the vmcnt window");
+  typedef typename MRVec<NK>::T vec;
+  constexpr int LPC = 64 / CP;
+  __shared__ __attribute__((aligned(16))) float gpart[2][M2_WAVES][NK * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int n0 = NK * lane;
+  float pr[NK], br[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    const int n = n0 + j;
+    pr[j] = n < N ? p[n] : 0.f;
+    br[j] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  const float invB = 1.0f / (float)Bv;
+  // per-class lane byte offsets (VGPRs, computed once, so the row base is the only scalar
+  // operand); lanes past ldN re-read the last vector (p = 0), classes c >= C re-read class
+  // C - 1 (masked in the softmax)
+  uint32_t cofs[CL];
+#pragma unroll
+  for (int c = 0; c < CL; ++c) cofs[c] = 4u * (uint32_t)(min(n0, ldN - NK) + min(c, C - 1) * ldN);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
+  // fetch cursor: the step whose row indices are read next (stays on the last step at the end)
+  int fst = 0, fep = 0, fsb = 0;
+  auto fetch_rows = [&](int& i0, int& i1) {
+    const int base = fep * nv + fsb * Bv;
+    const int bc = min(Bv, nv - fsb * Bv);
+    i0 = perms[base + (w < bc ? w : 0)];             // rows past the batch: its first row (masked)
+    i1 = perms[base + (w + M2_WAVES < bc ? w + M2_WAVES : 0)];
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+  };
+  vec zr[DEPTH][2][CL];
+  int idxq[DEPTH][2], labq[DEPTH][2];
+#define M2_LOAD(DST_, ROW_, C_)                                                                    \
+  {                                                                                                \
+    const int so_ = (ROW_) * CN * 4;                                                               \
+    if constexpr (NK == 1)                                                                         \
+      DST_ = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b32(zrs, cofs[C_], so_, 0));  \
+    else if constexpr (NK == 2)                                                                    \
+      DST_ = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b64(zrs, cofs[C_], so_, 0));  \
+    else                                                                                           \
+      DST_ = __builtin_bit_cast(vec, __builtin_amdgcn_raw_buffer_load_b128(zrs, cofs[C_], so_, 0)); \
+  }
+#define M2_ISSUE(R_, I0_, I1_)                                                             \
+  {                                                                                        \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                       \
+      M2_LOAD(zr[R_][0][c], I0_, c)                                                        \
+      M2_LOAD(zr[R_][1][c], I1_, c)                                                        \
+    }                                                                                      \
+  }
+  // prologue: rows and labels of steps 0 .. DEPTH-1 in flight, row indices of DEPTH .. 2 DEPTH-1
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) {
+    int i0, i1;
+    fetch_rows(i0, i1);
+    labq[k][0] = y[i0];
+    labq[k][1] = y[i1];
+    M2_ISSUE(k, i0, i1);
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) fetch_rows(idxq[k][0], idxq[k][1]);
+  // drain the prologue once, so the loop header inherits only the loop's own load order
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
+  int csb = 0;                                      // batch of step s within its epoch
+  int s = 0;
+#define M2_STEP(R_)                                                                        \
+  {                                                                                        \
+    if (s >= total) break;                                                                 \
+    const int bc = min(Bv, nv - csb * Bv);                                                 \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                   \
+    const bool ok0 = w < bc, ok1 = w + M2_WAVES < bc;                                      \
+    float v0[CP], v1[CP];                                                                  \
+    _Pragma("unroll") for (int c = 0; c < CP; ++c) {                                       \
+      float a = 0.f, b = 0.f;                                                              \
+      if (c < CL) {                                                                        \
+        _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                   \
+          a += mr_el<NK>(zr[R_][0][c], j) * pr[j];                                         \
+          b += mr_el<NK>(zr[R_][1][c], j) * pr[j];                                         \
+        }                                                                                  \
+      }                                                                                    \
+      v0[c] = a;                                                                           \
+      v1[c] = b;                                                                           \
+    }                                                                                      \
+    float o0, o1;                                                                          \
+    class_totals2<CP, SWAP>(v0, v1, lane, o0, o1);                                         \
+    const int cls = lane / LPC;                                                            \
+    const bool real = cls < C;                                                             \
+    const float m0 = class_max<LPC>(real ? o0 : -INFINITY, lane);                          \
+    const float m1 = class_max<LPC>(real ? o1 : -INFINITY, lane);                          \
+    const float e0 = class_sum<LPC>(real ? expf(o0 - m0) : 0.f, lane);                     \
+    const float e1 = class_sum<LPC>(real ? expf(o1 - m1) : 0.f, lane);                     \
+    const float invb = bc == Bv ? invB : 1.0f / (float)bc;                                 \
+    const float g0 = ok0 ? (cls == labq[R_][0] ? -invb : 0.f) + expf(o0 - m0 - logf(e0)) * invb : 0.f; \
+    const float g1 = ok1 ? (cls == labq[R_][1] ? -invb : 0.f) + expf(o1 - m1 - logf(e1)) * invb : 0.f; \
+    float gme[NK];                                                                         \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                           \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                       \
+      if (c < C) {                                                                         \
+        const float gc0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g0), c * LPC)); \
+        const float gc1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, g1), c * LPC)); \
+        _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                   \
+          gme[j] += gc0 * mr_el<NK>(zr[R_][0][c], j);                                      \
+          gme[j] += gc1 * mr_el<NK>(zr[R_][1][c], j);                                      \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+    const int par = s & 1;                                                                 \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[par][w][n0 + j] = gme[j];         \
+    /* the slot's rows are consumed: refill it with step s + DEPTH, label first */         \
+    labq[R_][0] = y[idxq[R_][0]];                                                          \
+    labq[R_][1] = y[idxq[R_][1]];                                                          \
+    M2_ISSUE(R_, idxq[R_][0], idxq[R_][1]);                                                \
+    lds_barrier();                 /* not __syncthreads: that would drain the ring */     \
+    fetch_rows(idxq[R_][0], idxq[R_][1]);       /* step s + 2 DEPTH */                     \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                       \
+      float gp = 0.f;                                                                      \
+      _Pragma("unroll") for (int i = 0; i < M2_WAVES; ++i) gp += gpart[par][i][n0 + j];    \
+      if (n0 + j < N) momentum_step(pr[j], br[j], gp, first, mom, lr);                     \
+    }                                                                                      \
+    first = 0;                                                                             \
+    ++s;                                                                                   \
+  }
+  for (;;) {
+    M2_STEP(0)
+    if constexpr (DEPTH > 1) M2_STEP(1)
+    if constexpr (DEPTH > 2) M2_STEP(2)
+  }
+#undef M2_STEP
+#undef M2_ISSUE
+#undef M2_LOAD
+  if (w == 0) {
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int n = n0 + j;
+      if (n < N) {
+        p[n] = pr[j];
+        buf[n] = br[j];
+      }
+    }
+    if (lane == 0 && total > 0) *first_flag = 0;
+  }
+}
+
+template <int NK, int CP, int CL>
+static void launch_mix_reg2(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                            int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                            int z_bytes, bool swap) {
+  constexpr int depth = 2 * CL * 3 <= 63 ? 3 : (2 * CL * 2 <= 63 ? 2 : 1);
+  if (swap)
+    hipLaunchKernelGGL((mix_solve_reg2_kernel<NK, CP, CL, depth, true>), dim3(1), dim3(M2_WAVES * 64), 0, st, Z, y,
+                       perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes);
+  else
+    hipLaunchKernelGGL((mix_solve_reg2_kernel<NK, CP, CL, depth, false>), dim3(1), dim3(M2_WAVES * 64), 0, st, Z, y,
+                       perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes);
+}
+
+// register-resident solver, form 2, for (N, C, Bv) if an instance covers it
+static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                           int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+  if (Bv > 2 * M2_WAVES || C > 10) return false;
+  const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
+  if (zb >= ((int64_t)1 << 31) || (int64_t)epochs * nv >= ((int64_t)1 << 31)) return false;   // 32-bit offsets
+  const char* sw = getenv("FS_MIX_SWAP");        // diagnostics: 0 = select-form reduce-scatter
+  const bool swap = !(sw && atoi(sw) == 0);
+  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : (N <= 256 ? 4 : 0));
+#define M2_CASE(NK_, CP_, CL_)                                                                              \
+  if (nk == NK_ && C <= CL_) {                                                                              \
+    launch_mix_reg2<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, (int)zb, swap); \
+    return true;                                                                                            \
+  }
+  M2_CASE(1, 2, 2) M2_CASE(1, 4, 4) M2_CASE(1, 8, 8) M2_CASE(1, 16, 10)
+  M2_CASE(2, 2, 2) M2_CASE(2, 4, 4) M2_CASE(2, 8, 8) M2_CASE(2, 16, 10)
+  M2_CASE(4, 2, 2) M2_CASE(4, 4, 4)
+#undef M2_CASE
+  return false;
+}
+
+// ----------------------------------------------------------------------------
 // p-solve, multi-CU form (Bv <= 16, C <= 16, N <= 2048).  One workgroup on one CU cannot
 // stream a batch of Z rows faster than ~33 GB/s (gathered rows from the Infinity Cache,
 // MI355X_MICROARCH.md "Indexed rows"): at config 2 that is 64 KB per step, ~2 us -- the
@@ -811,13 +1065,19 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
   FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
   hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
-  // solver choice: FS_MIX_SOLVER=auto (default) | mc | reg | staged | global (diagnostics
+  // solver choice: FS_MIX_SOLVER=auto (default) | reg2 | reg | mc | staged | global (diagnostics
   // and tests; a forced solver that does not cover the shape falls through to the next one)
   const char* pick = getenv("FS_MIX_SOLVER");
   const std::string want = pick ? pick : "auto";
   // auto: the single-CU register solver where an instance covers the shape (no cross-CU
   // exchange: ~1-2.5 us per step), else the multi-CU solver (~4-7 us per step, 7-11x the
   // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
+  if ((want == "auto" || want == "reg2") &&
+      mix_solve_reg2(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
+    t_last_solver = 5;
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
   if ((want == "auto" || want == "reg") &&
       mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
     t_last_solver = 1;

@@ -37,7 +37,8 @@ for rep in range(3):
     L.check(L.lib().fs_mix_z(L.ptr(W), L.ptr(mix.f.phi), mix.f.ld, N, C, nv, L.ptr(mix.Z), L.stream_ptr()), 'z')
     e1.record()
     L.check(L.lib().fs_mix_solve(L.ptr(mix.Z), L.ptr(mix.f.labels), L.ptr(perms), N, C, nv, ep, 16, 1e-3, 0.9,
-                                 L.ptr(mix.p), L.ptr(mix.buf), L.ptr(mix.first), L.stream_ptr()), 'solve')
+                                 L.ptr(mix.p), L.ptr(mix.buf), L.ptr(mix.first), L.ptr(mix.ws), mix.ws.numel(),
+                                 L.stream_ptr()), 'solve')
     e2.record()
     torch.cuda.synchronize()
     ts.append((e0.elapsed_time(e1), e1.elapsed_time(e2)))
@@ -46,8 +47,9 @@ zms, sms = ts[-1]
 print('N=%d C=%d n_val=%d epochs=%d: mix_z %.1f us (%.1f TFLOP/s), mix_solve %.2f ms = %.3f us/step over %d steps; '
       'p finite: %s' % (N, C, nv, ep, zms * 1e3, 2.0 * N * C * D * nv / zms / 1e9, sms, sms * 1e3 / steps, steps,
                         bool(torch.isfinite(mix.p).all())), flush=True)
-print('  solver %s, multi-CU state %d (0 = not run, 1 = ran, +4 = spin timeout)'
-      % (os.environ.get('FS_MIX_SOLVER', 'auto'), L.lib().fs_mix_solve_last_mode()), flush=True)
+mix.check_errors()
+print('  solver requested %s, ran %s' % (os.environ.get('FS_MIX_SOLVER', 'auto'),
+                                         L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]), flush=True)
 if STAMPS:
     acc = mix.buf[N + 8:N + 18].cpu().numpy().view(np.uint64)
     names = ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update']

@@ -175,8 +175,7 @@ def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
     parallel, 4-wave (two workgroups per CU) and 8-wave workgroups, against the oracle:
     D = 1000 (16 tiles, the last one ragged), C = 10, tail batches of 1 and 7 rows, and a
     client with no rows (its result is its start)."""
-    if nw == 8:
-        monkeypatch.setenv('FS_SPLIT_NW', '8')
+    monkeypatch.setenv('FS_SPLIT_NW', str(nw))     # 4-wave workgroups are opt-in (the planner picks 8)
     rs = np.random.RandomState(G + 10 * chained + 100 * prox)
     D, C, B, E = 1000, 10, 32, 2
     sizes = [65, 33, 0, 7, 96, 40]
@@ -275,8 +274,10 @@ def test_eval_unit_golden(amd):
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [
-    (10, 2, 203, 16),       # config 1 shape: register solver, NK=1, CP=2
+    (10, 2, 203, 16),       # config 1 shape: register solver form 2, NK=1, CP=2
     (100, 10, 517, 16),     # config 2 shape: NK=2, CP=16 (10 loaded classes)
+    (200, 4, 301, 16),      # NK=4, CP=4 (at lr 0.1: lr 0.5 makes this p-SGD ill-conditioned, fp32 vs fp64 2e-4)
+    (60, 8, 33, 9),         # CP=8, 9-row batches: the second row of every wave idles
     (64, 7, 130, 16),       # N exactly one lane per client
     (129, 3, 77, 8),        # NK=4, Bv < 16 (idle waves), ragged last batch
     (37, 20, 90, 16),       # C > 16: CP=32, 2-deep ring
@@ -285,7 +286,10 @@ def test_eval_unit_golden(amd):
     (300, 4, 60, 16),       # N > 256: multi-CU solver
 ])
 def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
-    """fs_mix_solve (every solver variant it selects) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    """fs_mix_solve (every solver variant it selects) vs the oracle's p-SGD, 2 rounds x 2 epochs.
+    Every case is well-conditioned: the fp32 oracle is within 5e-6 of an fp64 run of it."""
+    if (N, C, nv) == (200, 4, 301):
+        lr = 0.1
     rs = np.random.RandomState(N + C + nv)
     D = 64
     Ws = (rs.normal(size=(N, C, D)) * 0.5).astype(np.float32)
@@ -304,8 +308,9 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         mix.check_errors()
         torch.manual_seed(70 + rnd)
         pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, lr, 2, batch_size=Bv)
-        assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
-        assert np.abs(mix.buf.cpu().numpy() - br).max() <= 1e-4 * np.abs(br).max()
+        ep = float(np.abs(mix.p.cpu().numpy() - pr).max() / np.abs(pr).max())
+        eb = float(np.abs(mix.buf.cpu().numpy() - br).max() / np.abs(br).max())
+        assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
 @pytest.mark.parametrize('N,C,nv,Bv,S', [
@@ -333,11 +338,17 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
 
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
-                                        ('mc', 1000, 7)])
+                                        ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('reg2-select', 100, 10),
+                                        ('reg2-select', 129, 3)])
 def test_mix_solve_forced_fallbacks(amd, monkeypatch, solver, N, C):
-    """The solvers the auto choice does not take at these shapes."""
+    """The solvers the auto choice does not take at these shapes (reg2-select: form 2 with the
+    select-form reduce-scatter instead of the permlane swap-add levels)."""
+    if solver == 'reg2-select':
+        monkeypatch.setenv('FS_MIX_SWAP', '0')
+        solver = 'reg2'
     monkeypatch.setenv('FS_MIX_SOLVER', solver)
     test_mix_solve_variants(amd, N, C, 133, 16, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
 
 
 def test_mix_z_and_solve_vs_oracle(amd):
@@ -365,8 +376,9 @@ def test_mix_z_and_solve_vs_oracle(amd):
             pr, br = O.mixture_solve(list(Ws), Xv, yv, p0, None, 0.05, 3)
         else:
             pr, br = O.mixture_solve(list(Ws), Xv, yv, pr, br, 0.05, 3)
-        assert np.abs(mix.p.cpu().numpy() - pr).max() <= 1e-5 * np.abs(pr).max()
-        assert np.abs(mix.buf.cpu().numpy() - br).max() <= 1e-4 * np.abs(br).max()
+        ep = float(np.abs(mix.p.cpu().numpy() - pr).max() / np.abs(pr).max())
+        eb = float(np.abs(mix.buf.cpu().numpy() - br).max() / np.abs(br).max())
+        assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
 # ----------------------------------------------------------------------------- full size
