@@ -828,9 +828,30 @@ constexpr int MC_THREADS = 256;
 constexpr int MC_XCDS = 8;
 constexpr int MC_KMAX = 32;
 constexpr int MC_SLOT = 256;                     // granules per workgroup per parity
+constexpr int MC_TOT = 256;                      // hop-2 granules (logit totals) per parity
 constexpr unsigned MC_SPIN_LIMIT = 1u << 20;
 
-template <int S>
+// spin on one granule until it carries `tag`; false (and the error word set) on a timeout
+__device__ __forceinline__ bool mc_wait(const unsigned long long* g, unsigned tag, unsigned long long& out,
+                                        unsigned spin_limit, unsigned* err) {
+  unsigned spins = 0;
+  for (;;) {
+    out = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(out >> 32) == tag) return true;
+    if (++spins > spin_limit) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+// HOPS = 1: every workgroup reads all K partial vectors (16 C K granules per workgroup and
+// step).  HOPS = 2: reduce-scatter + all-gather -- value r = b*C + c of the 16 x C logits is
+// owned by workgroup r % K, which folds the K partials of its ceil(16C/K) values in workgroup
+// order (the same left fold as HOPS = 1, so the same bits) and publishes the totals; every
+// workgroup then reads the 16 C totals.  About 2 x 16 C granules per workgroup and step
+// instead of 16 C K: at K = 32 the exchange no longer out-reads the Z slice.
+template <int S, int HOPS>
 __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* __restrict__ Z,
                                                                  const int32_t* __restrict__ y,
                                                                  const int32_t* __restrict__ perms, int N, int C,
@@ -841,10 +862,12 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
                                                                  unsigned* __restrict__ err, int K,
                                                                  unsigned spin_limit) {
   static_assert(S == 8 || S == 16 || S == 32 || S == 64, "slice width");
+  static_assert(HOPS == 1 || HOPS == 2, "exchange form");
   if (blockIdx.x % MC_XCDS) return;
   constexpr int LPV = 64 / S;                      // lanes per value after the reduce-scatter
   __shared__ __attribute__((aligned(16))) float ps[S];
   __shared__ float gp[MC_THREADS / 64][S];
+  __shared__ float part[HOPS == 2 ? 2 * MC_THREADS : 1];   // hop 1: partials of owned values
   const int k = blockIdx.x / MC_XCDS;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int b = t >> 4, c = t & 15;
@@ -912,30 +935,65 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
     unsigned long long* slot = xbuf + (int64_t)(st & 1) * K * MC_SLOT;
     const bool real = c < C;
     float o = 0.f;
-    if (real) {
+    if (real)
       __hip_atomic_store(slot + (int64_t)k * MC_SLOT + t,
                          ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(a), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-      unsigned long long gr[MC_KMAX];
-      unsigned spins = 0;
-      for (;;) {
+    if constexpr (HOPS == 1) {
+      if (real) {
+        unsigned long long gr[MC_KMAX];
+        unsigned spins = 0;
+        for (;;) {
+#pragma unroll
+          for (int q = 0; q < MC_KMAX; ++q)
+            if (q < K) gr[q] = __hip_atomic_load(slot + (int64_t)q * MC_SLOT + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bool ok = true;
+#pragma unroll
+          for (int q = 0; q < MC_KMAX; ++q)
+            if (q < K) ok = ok && (unsigned)(gr[q] >> 32) == tag;
+          if (ok || dead) break;
+          if (++spins > spin_limit) {
+            dead = true;
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
 #pragma unroll
         for (int q = 0; q < MC_KMAX; ++q)
-          if (q < K) gr[q] = __hip_atomic_load(slot + (int64_t)q * MC_SLOT + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
+          if (q < K) o += __uint_as_float((unsigned)gr[q]);
+      }
+    } else {
+      // hop 1: this workgroup owns values r = k + K i; thread u loads partner q = u % K's
+      // partial of owned value i = u / K (two passes when 16 C + K > 256)
+      const int nval = 16 * C;
+      const int nown = (nval - k + K - 1) / K;     // values r = k + K i < 16 C
+      unsigned long long* tots = xbuf + (int64_t)2 * K * MC_SLOT + (int64_t)(st & 1) * MC_TOT;
 #pragma unroll
-        for (int q = 0; q < MC_KMAX; ++q)
-          if (q < K) ok = ok && (unsigned)(gr[q] >> 32) == tag;
-        if (ok || dead) break;
-        if (++spins > spin_limit) {
-          dead = true;
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+      for (int pass = 0; pass < 2; ++pass) {
+        const int u = t + pass * MC_THREADS;
+        const int i = u / K, q = u - (u / K) * K;
+        if (i < nown) {
+          const int r = k + K * i;
+          const int tr = (r / C) * 16 + (r % C);   // thread slot of value r in a partial vector
+          unsigned long long gv = 0;
+          if (!dead && !mc_wait(slot + (int64_t)q * MC_SLOT + tr, tag, gv, spin_limit, err)) dead = true;
+          part[u] = __uint_as_float((unsigned)gv);
         }
       }
-#pragma unroll
-      for (int q = 0; q < MC_KMAX; ++q)
-        if (q < K) o += __uint_as_float((unsigned)gr[q]);
+      lds_barrier();
+      if (t < nown) {                              // fold in workgroup order, publish the total
+        float sum = 0.f;
+        for (int q = 0; q < K; ++q) sum += part[t * K + q];
+        const int r = k + K * t;
+        __hip_atomic_store(tots + r, ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(sum),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // hop 2: every real thread reads the total of its own value
+      if (real) {
+        unsigned long long gv = 0;
+        if (!dead && !mc_wait(tots + (b * C + c), tag, gv, spin_limit, err)) dead = true;
+        o = __uint_as_float((unsigned)gv);
+      }
     }
     // ---- softmax-CE gradient of row b (16-lane class groups) ----
     const int sb = st % nbat;
@@ -984,7 +1042,14 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
 // before every launch) followed by a 256-byte error block (sticky: only the caller clears it)
 constexpr int64_t MC_ERR_BYTES = 256;
 
-static int64_t mc_xbytes(int K) { return (int64_t)sizeof(unsigned long long) * 2 * K * MC_SLOT; }
+static int64_t mc_xbytes(int K) { return (int64_t)sizeof(unsigned long long) * 2 * (K * MC_SLOT + MC_TOT); }
+
+// exchange form: FS_MIX_MC_HOPS=1|2 (diagnostics); default two hops from K = 8 workgroups
+static int mc_hops(int K) {
+  const char* env = getenv("FS_MIX_MC_HOPS");
+  if (env && (atoi(env) == 1 || atoi(env) == 2)) return atoi(env);
+  return K >= 8 ? 2 : 1;
+}
 
 static unsigned mc_spin_limit() {
   const char* s = getenv("FS_SPIN_LIMIT");        // test knob: 0 injects an exchange timeout
@@ -1021,11 +1086,13 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
   const unsigned spin_limit = mc_spin_limit();
   const dim3 grid(MC_XCDS * K), block(MC_THREADS);
-#define MC_CASE(S_)                                                                                        \
-  if (S == S_)                                                                                             \
-    hipLaunchKernelGGL(mix_solve_mc_kernel<S_>, grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, \
-                       buf, first, ws, err, K, spin_limit);
-  MC_CASE(8) MC_CASE(16) MC_CASE(32) MC_CASE(64)
+  const int hops = mc_hops(K);
+#define MC_CASE(S_, H_)                                                                                      \
+  if (S == S_ && hops == H_)                                                                                 \
+    hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, \
+                       p, buf, first, ws, err, K, spin_limit);
+  MC_CASE(8, 1) MC_CASE(16, 1) MC_CASE(32, 1) MC_CASE(64, 1)
+  MC_CASE(8, 2) MC_CASE(16, 2) MC_CASE(32, 2) MC_CASE(64, 2)
 #undef MC_CASE
   return 0;
 }
@@ -1072,7 +1139,9 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // auto: the single-CU register solver where an instance covers the shape (no cross-CU
   // exchange: ~1-2.5 us per step), else the multi-CU solver (~4-7 us per step, 7-11x the
   // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
-  if ((want == "auto" || want == "reg2") &&
+  // form 2 (two rows per wave) where it measured faster: N in (128, 256], NK = 4 (2.0 vs 4.1 us
+  // per step at N = 256, C = 4); below that the one-row form is as fast or faster (r02g)
+  if (((want == "auto" && N > 128) || want == "reg2") &&
       mix_solve_reg2(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
     t_last_solver = 5;
     FS_LAUNCH_CHECK();

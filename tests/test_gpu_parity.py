@@ -313,6 +313,7 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
+@pytest.mark.parametrize('hops', [1, 2])
 @pytest.mark.parametrize('N,C,nv,Bv,S', [
     (100, 10, 517, 16, None),   # config 2 shape: S = 8, K = 13 workgroups
     (100, 10, 517, 16, 32),     # same, 4 workgroups of 32 clients
@@ -324,10 +325,12 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
     (5, 2, 40, 16, 8),          # one workgroup (K = 1)
     (1100, 16, 40, 16, None),   # S = 64, C = 16
 ])
-def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S):
-    """fs_mix_solve's multi-CU solver (clients split over K workgroups, one partial-logit
-    exchange per step) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S, hops):
+    """fs_mix_solve's multi-CU solver (clients split over K workgroups, partial-logit exchange
+    every step: one hop, or reduce-scatter + all-gather) vs the oracle's p-SGD, 2 rounds x 2
+    epochs."""
     monkeypatch.setenv('FS_MIX_SOLVER', 'mc')
+    monkeypatch.setenv('FS_MIX_MC_HOPS', str(hops))
     if S:
         monkeypatch.setenv('FS_MIX_MC_S', str(S))
     # (at N >= 1000, lr_p = 0.5 drives p to |p| ~ 10 within a few steps, where any two fp32
