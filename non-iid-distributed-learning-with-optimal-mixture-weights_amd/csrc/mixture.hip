@@ -851,7 +851,11 @@ __device__ __forceinline__ bool mc_wait(const unsigned long long* g, unsigned ta
 // order (the same left fold as HOPS = 1, so the same bits) and publishes the totals; every
 // workgroup then reads the 16 C totals.  About 2 x 16 C granules per workgroup and step
 // instead of 16 C K: at K = 32 the exchange no longer out-reads the Z slice.
-template <int S, int HOPS>
+// ZAT: where the next step's Z slice is issued -- 0 at the top of the step (it streams while
+// the exchange waits, but every poll queues behind it: a hop between streaming CUs costs ~3x
+// an idle one, MI355X_MICROARCH.md handoff-1to1), 1 after hop 1 (HOPS = 2: hop 1 runs with
+// an empty queue), 2 after the exchange (both hops idle, the slice's latency exposed).
+template <int S, int HOPS, int ZAT>
 __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* __restrict__ Z,
                                                                  const int32_t* __restrict__ y,
                                                                  const int32_t* __restrict__ perms, int N, int C,
@@ -913,12 +917,14 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
   for (int st = 0; st < total; ++st) {
     // ---- next step's slice streams behind this step ----
     float4 zn[S / 4];
-    {
+    int yn = 0;
+    auto issue_next = [&]() {
       const float* zr = Z + (int64_t)vnext * CN;
 #pragma unroll
       for (int i = 0; i < S / 4; ++i) zn[i] = ld4(zr + coff[i]);
-    }
-    const int yn = y[vnext];
+      yn = y[vnext];
+    };
+    if constexpr (ZAT == 0 || (ZAT == 1 && HOPS == 1)) issue_next();
     const int vn2 = row_at(st + 2);
     // ---- partial logits of this workgroup's clients ----
     float a = 0.f;
@@ -980,6 +986,7 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
           part[u] = __uint_as_float((unsigned)gv);
         }
       }
+      if constexpr (ZAT == 1) issue_next();
       lds_barrier();
       if (t < nown) {                              // fold in workgroup order, publish the total
         float sum = 0.f;
@@ -995,6 +1002,7 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
         o = __uint_as_float((unsigned)gv);
       }
     }
+    if constexpr (ZAT == 2) issue_next();
     // ---- softmax-CE gradient of row b (16-lane class groups) ----
     const int sb = st % nbat;
     const int bc = min(Bv, nv - sb * Bv);
@@ -1087,12 +1095,20 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   const unsigned spin_limit = mc_spin_limit();
   const dim3 grid(MC_XCDS * K), block(MC_THREADS);
   const int hops = mc_hops(K);
-#define MC_CASE(S_, H_)                                                                                      \
-  if (S == S_ && hops == H_)                                                                                 \
-    hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, \
-                       p, buf, first, ws, err, K, spin_limit);
-  MC_CASE(8, 1) MC_CASE(16, 1) MC_CASE(32, 1) MC_CASE(64, 1)
-  MC_CASE(8, 2) MC_CASE(16, 2) MC_CASE(32, 2) MC_CASE(64, 2)
+  // Z-slice issue point (FS_MIX_MC_ZAT=0|1|2 for diagnostics): after the exchange by default --
+  // r02i, us per step, (hops, ZAT) = (1, 0) / (2, 0) / (2, 1) / (2, 2): N = 1000, C = 10, K = 32:
+  // 6.61 / 6.03 / 5.45 / 5.44; N = 300, C = 4, K = 19: 4.33 / 4.34 / 4.08 / 3.38
+  const char* zenv = getenv("FS_MIX_MC_ZAT");
+  const int zat = zenv ? std::min(2, std::max(0, atoi(zenv))) : 2;
+#define MC_CASE(S_, H_, Z_)                                                                                   \
+  if (S == S_ && hops == H_ && zat == Z_)                                                                     \
+    hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_, Z_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, \
+                       mom, p, buf, first, ws, err, K, spin_limit);
+#define MC_CASES(Z_) \
+  MC_CASE(8, 1, Z_) MC_CASE(16, 1, Z_) MC_CASE(32, 1, Z_) MC_CASE(64, 1, Z_) \
+  MC_CASE(8, 2, Z_) MC_CASE(16, 2, Z_) MC_CASE(32, 2, Z_) MC_CASE(64, 2, Z_)
+  MC_CASES(0) MC_CASES(1) MC_CASES(2)
+#undef MC_CASES
 #undef MC_CASE
   return 0;
 }
