@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 5
+#define FS_ABI_VERSION 6
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -242,6 +242,10 @@ typedef struct fs_plan_desc {
   int shuffle_device;          /* 1: replay shuffles with fs_randperm_device on the plan's side
                                   stream; 0: on the plan's host thread pool + async upload */
   int host_threads;            /* host replay threads; <= 0: min(16, hardware) */
+  int shuffle_after_train;     /* 1 (device replay): round t+1's shuffles also wait for round t's
+                                  local training, so they run beside what follows it (FedAMW: the
+                                  p-solve, which leaves most CUs idle) instead of holding CUs a
+                                  group of the split kernel is waiting for */
 } fs_plan_desc;
 
 int64_t fs_plan_desc_size(void);   /* sizeof(fs_plan_desc), for binding-layout checks */

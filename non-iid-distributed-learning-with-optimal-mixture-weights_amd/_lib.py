@@ -50,7 +50,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
@@ -69,6 +69,7 @@ class PlanDesc(C.Structure):
         ('d_p', C.c_void_p), ('d_agg_ws', C.c_void_p), ('agg_ws_floats', C.c_int64), ('agg_chunks', C.c_int),
         ('d_phi_t', C.c_void_p), ('d_labels_t', C.c_void_p), ('n_t', C.c_int), ('d_eval_ws', C.c_void_p),
         ('d_eval_hist', C.c_void_p), ('shuffle_device', C.c_int), ('host_threads', C.c_int),
+        ('shuffle_after_train', C.c_int),
     ]
 
 _lib = None

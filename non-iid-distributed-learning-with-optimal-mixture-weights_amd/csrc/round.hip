@@ -266,6 +266,9 @@ static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   if (p->up_pending[s]) FS_HIP(hipEventSynchronize(p->uploaded[s]), "fs_plan_shuffle");   // pinned seeds free
   std::memcpy(p->h_seed[s], h_seeds, sizeof(int64_t) * P);
   if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
+  // optionally also behind the latest local training (the other slot's consumer)
+  if (p->d.shuffle_after_train && p->cons_recorded[s ^ 1])
+    FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s ^ 1], 0), "fs_plan_shuffle");
   FS_HIP(hipMemcpyAsync(p->d_seed[s], p->h_seed[s], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
          "fs_plan_shuffle");
   const int rc = fs_randperm_device(p->d_seed[s], p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], p->copy);

@@ -211,7 +211,8 @@ class RoundPlan:
     Borrows every device buffer from the objects passed in (they must outlive it)."""
 
     def __init__(self, trainer, W_g, loss_hist, p=None, aggregator=None, evaluator=None, eval_hist=None,
-                 prox=False, mu=0.0, reg=False, lam=0.0, chained=False, shuffle_device=True, host_threads=0):
+                 prox=False, mu=0.0, reg=False, lam=0.0, chained=False, shuffle_device=True, host_threads=0,
+                 shuffle_after_train=False):
         import ctypes
         f = trainer.f
         self._keep = [trainer, W_g, loss_hist, p, aggregator, evaluator, eval_hist]
@@ -235,6 +236,7 @@ class RoundPlan:
             d.d_eval_ws, d.d_eval_hist = evaluator.ws.data_ptr(), eval_hist.data_ptr()
         d.shuffle_device = int(bool(shuffle_device))
         d.host_threads = int(host_threads)
+        d.shuffle_after_train = int(bool(shuffle_after_train))
         self._desc = d
         self._h = ctypes.c_void_p()
         _lib.check(_lib.lib().fs_plan_create(ctypes.byref(d), ctypes.byref(self._h)), 'fs_plan_create')

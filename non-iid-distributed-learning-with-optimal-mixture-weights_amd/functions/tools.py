@@ -181,7 +181,11 @@ class Federation:
                                      aggregator=self.agg if self.mixture is None else None,
                                      evaluator=self.evaluator, eval_hist=self.eval_hist, prox=prox, mu=mu,
                                      reg=lambda_reg_if, lam=lambda_reg, chained=self.chained,
-                                     shuffle_device=shuffle_device)
+                                     shuffle_device=shuffle_device, shuffle_after_train=self.mixture is not None)
+        # FedAMW: round t+1's shuffles (training and validation passes) are generated behind
+        # round t's local training, beside its p-solve (one to 32 CUs busy), not beside the
+        # training kernel, whose groups would wait for the CUs they hold
+        self._train_done = None
         self.t = 0
         self.events = None              # a list: round() appends (phase, start, end) HIP timing events
 
@@ -193,6 +197,8 @@ class Federation:
         seeds = rng.draw_pass_seeds(N * E + self.n_val_pass + 1)
         self.plan.shuffle(seeds[:N * E].reshape(N, E)[self.mine].reshape(-1), t)
         if self.mixture is not None:
+            if self._train_done is not None:
+                self.side.wait_event(self._train_done)
             self.mixture.prepare(seeds[N * E:N * E + self.n_val_pass], t % 2, self.side)
 
     def round(self):
@@ -218,6 +224,9 @@ class Federation:
             return out
 
         timed('train', lambda: self.plan.round(t, self.lr, P[0]))
+        if self.mixture is not None:
+            self._train_done = torch.cuda.Event()
+            self._train_done.record()
         if self.zshard:
             # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
