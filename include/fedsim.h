@@ -144,7 +144,9 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * torch.optim.SGD starts empty, tools.py:423).  A single persistent workgroup
  * where a register-resident instance covers (N, C, Bv); otherwise (Bv <= 16,
  * C <= 16, N <= 2048) K <= 32 workgroups that split the clients and exchange
- * partial logits once per step; otherwise one LDS-staged / global workgroup.
+ * partial logits every step (slices of S >= 16 clients: reduce-scatter to owner workgroups, then an
+ * all-gather of the totals; FS_MIX_MC_HOPS=1 forces the one-hop all-to-all);
+ * otherwise one LDS-staged / global workgroup.
  * d_ws: fs_mix_solve_ws_bytes(N, C, Bv) bytes, zeroed once at allocation (the multi-CU
  * exchange granules + the error block; a timed-out exchange also writes NaN into d_p).
  * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=reg2|reg|mc|staged|global

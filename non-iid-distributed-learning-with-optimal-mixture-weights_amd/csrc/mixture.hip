@@ -1052,11 +1052,13 @@ constexpr int64_t MC_ERR_BYTES = 256;
 
 static int64_t mc_xbytes(int K) { return (int64_t)sizeof(unsigned long long) * 2 * (K * MC_SLOT + MC_TOT); }
 
-// exchange form: FS_MIX_MC_HOPS=1|2 (diagnostics); default two hops from K = 8 workgroups
-static int mc_hops(int K) {
+// exchange form: FS_MIX_MC_HOPS=1|2 (diagnostics).  Default two hops, except at S = 8 -- r02n,
+// N = 100, C = 10, us per step, one hop / two hops (Z issued after the exchange): S = 64 (K = 2)
+// 5.50 / 4.14, S = 32 (K = 4) 4.43 / 2.90, S = 16 (K = 7) 3.95 / 2.87, S = 8 (K = 13) 3.25 / 3.79
+static int mc_hops(int K, int S) {
   const char* env = getenv("FS_MIX_MC_HOPS");
   if (env && (atoi(env) == 1 || atoi(env) == 2)) return atoi(env);
-  return K >= 8 ? 2 : 1;
+  return (K >= 2 && S >= 16) ? 2 : 1;
 }
 
 static unsigned mc_spin_limit() {
@@ -1094,7 +1096,7 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
   const unsigned spin_limit = mc_spin_limit();
   const dim3 grid(MC_XCDS * K), block(MC_THREADS);
-  const int hops = mc_hops(K);
+  const int hops = mc_hops(K, S);
   // Z-slice issue point (FS_MIX_MC_ZAT=0|1|2 for diagnostics): after the exchange by default --
   // r02i, us per step, (hops, ZAT) = (1, 0) / (2, 0) / (2, 1) / (2, 2): N = 1000, C = 10, K = 32:
   // 6.61 / 6.03 / 5.45 / 5.44; N = 300, C = 4, K = 19: 4.33 / 4.34 / 4.08 / 3.38
