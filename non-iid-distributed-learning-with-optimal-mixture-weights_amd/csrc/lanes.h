@@ -39,7 +39,8 @@ __device__ __forceinline__ float xor_get(float x, int off, int lane) {
 // one reduce-scatter level over lane pairs (l, l ^ off): lanes with (lane & off) keep the
 // upper element `b`, the others the lower `a`; returns keep + partner's copy of it.
 // (Summing both outputs of one permlane swap of (a, b) would save the selects, but this
-// compiler folds that sum to r0 + r0 -- verified by scripts/probe/xorget.hip.)
+// compiler folds that sum to r0 + r0 -- verified by scripts/probe/xorget.hip; mixture.hip's
+// rs_level issues the swap as inline asm instead, where both outputs survive.)
 __device__ __forceinline__ float rs_pair(float a, float b, int off, int lane) {
   const bool h = (lane & off) != 0;
   return (h ? b : a) + xor_get(h ? a : b, off, lane);
@@ -61,6 +62,14 @@ __device__ __forceinline__ float class_totals(float (&v)[CP], int lane) {
   for (int off = LPC / 2; off >= 1; off >>= 1) o += xor_get(o, off, lane);
   return o;
 }
+// wave-wide sum, xor butterfly 32 .. 1 (the same order, so the same bits, as the ds_bpermute
+// form of common.h's wave_sum); every lane must be active
+__device__ __forceinline__ float wave_sum_dpp(float v, int lane) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += xor_get(v, off, lane);
+  return v;
+}
+
 // max / sum over the class groups of a class_totals layout (lanes l, l^LPC, l^2LPC, ...)
 template <int LPC>
 __device__ __forceinline__ float class_max(float x, int lane) {

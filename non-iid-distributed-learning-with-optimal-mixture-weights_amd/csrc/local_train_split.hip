@@ -32,6 +32,7 @@
 // Hand-off tags are the group's step counter + 1 (32 bits): the exchange buffer is zeroed by
 // the launcher before every launch.
 #include "common.h"
+#include "lanes.h"
 
 namespace fs {
 
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
         s += wr[i][q].x * wr[i][q].x + wr[i][q].y * wr[i][q].y + wr[i][q].z * wr[i][q].z + wr[i][q].w * wr[i][q].w;
       }
     }
-    return wave_sum(s);
+    return wave_sum_dpp(s, lane);
   };
   auto store_w = [&](float* Wj) {
     const int64_t base = wbase();
@@ -462,12 +463,14 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
         const int r = idx / NC, c = idx - r * NC;
         const bool valid = r < bc && c < C;
         const float z = valid ? zsum[r][c] : 0.f;
+        // (the loop is wave-uniform -- NZ is a multiple of 64 -- so the DPP exchanges run with
+        // every lane active)
         float m = valid ? z : -INFINITY;
 #pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
         float se = valid ? expf(z - m) : 0.f;
 #pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) se += __shfl_xor(se, off, 64);
+        for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
         float gv = 0.f;
         if (valid) {
           const float lp = z - m - logf(se);
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
         }
         gbuf[r][c] = gv;
       }
-      cep = wave_sum(cep);
+      cep = wave_sum_dpp(cep, lane);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
       if ((SCHED == 0 && w >= NW / 2) || (SCHED == 1 && w < NW / 2)) SP_NEXT();
@@ -537,8 +540,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
           }
         }
       }
-      npn = wave_sum(npn);
-      nwn = wave_sum(nwn);
+      npn = wave_sum_dpp(npn, lane);
+      nwn = wave_sum_dpp(nwn, lane);
       if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
       SP_STAMP(8)
     }
@@ -636,15 +639,18 @@ static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t
   hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED, NW>), dim3(grid), dim3(NW * 64), lds, st, P, X);
 }
 
-static int split_sched(int G, int NW) {
+// default: 1 where half the waves streaming during the hand-off pays (parallel clients, G <= 8:
+// config 2 24.2k vs 25.7k cycles per step); 0 for chained clients (32 KB per CU per step:
+// config 1 at G = 8 13.8k vs 14.8k), G = 16 and 4-wave workgroups
+static int split_sched(int G, int NW, bool chained) {
   const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
   if (s) return std::max(0, std::min(1, atoi(s)));
-  return (G >= 16 || NW == 4) ? 0 : 1;           // (4-wave hand-off threads: all of them)
+  return (chained || G >= 16 || NW == 4) ? 0 : 1;  // (4-wave hand-off threads: all of them)
 }
 
 template <int RT, int G, bool PROX>
 static void launch_split_p(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
-  const int sc = split_sched(G, NW);
+  const int sc = split_sched(G, NW, P.chained != 0);
   if constexpr (G >= 16) {
     launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);     // the hand-off values need all 512 threads
   } else {
