@@ -31,6 +31,8 @@
 // every spin is bounded and a timeout is reported through the workspace error word.
 // Hand-off tags are the group's step counter + 1 (32 bits): the exchange buffer is zeroed by
 // the launcher before every launch.
+#include <type_traits>
+
 #include "common.h"
 #include "lanes.h"
 
@@ -126,6 +128,10 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 //   1  the second half writes its image slice and issues its next rows at once (their bytes
 //      stream during the hand-off); the first half alone runs the hand-off (nothing of its
 //      own queued ahead of its polls) and issues its rows after the softmax.
+//   2  every wave runs the hand-off; no wave issues its next rows in a burst: each issues
+//      one row load per backward iteration (16 per wave per step), so the issue stalls of a
+//      full memory queue land between the backward's MFMAs instead of ahead of them.
+//   3  as 1 for the second half; the first half interleaves its rows into the backward as 2.
 template <int RT, int G, bool PROX, int SCHED, int NWV>
 __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_kernel(LTParams P, SplitWS X) {
   constexpr int NW = NWV;
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
-  constexpr int XT = SCHED ? NTH / 2 : NTH;       // threads running the hand-off
+  constexpr int XT = (SCHED == 1 || SCHED == 3) ? NTH / 2 : NTH;   // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
   constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
   constexpr int HC = G;                             // partners polled per round trip
@@ -363,7 +369,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
 
-      const bool xw = SCHED == 0 || w < NW / 2;      // this wave runs the hand-off
+      const bool xw = SCHED == 0 || SCHED == 2 || w < NW / 2;   // this wave runs the hand-off
       if (!xw) {
         SP_IMG_WRITE();
         SP_NEXT();
@@ -506,10 +512,17 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       const float lr = P.lr;
       const int rblk = 4 * (l16 & 3) + (l16 >> 2);
       float npn = 0.f, nwn = 0.f;
+      // schedules 2 / 3: this wave's next rows go out one load per backward iteration
+      const bool ilv = lc_ok && (SCHED == 2 || (SCHED == 3 && w < NW / 2));
+      // (two instances, so the interleaved loads are straight-line code: a branch around each
+      // load would make the compiler wait for it at the join)
+      // FULL: every wave owns TPW tiles (NTS = NW * TPW, every BASELINE shape but chained config
+      // 1), so no tile guard splits the block either
+      auto bwd = [&](auto LD, auto FULL) {
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         const int Tl = w + NW * i;
-        if (Tl < NTS) {
+        if (decltype(FULL)::value || Tl < NTS) {
           floatx4 ga[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) ga[e4] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -518,6 +531,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
             const float4 x = ld4(xs_lds + img_off(4 * kk + lg, RS, Tl, rblk));
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
+            if constexpr (decltype(LD)::value)
+              xf[i][kk >> 2][kk & 3] = ld4(P.phi + (int64_t)pn[kk >> 2] * ld + 64 * t0 + 4 * lg + 64 * Tl + 16 * (kk & 3));
           }
           if (l16 < C) {
 #pragma unroll
@@ -539,6 +554,22 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
             }
           }
         }
+      }
+      };
+      if (ilv) {
+        if (NTS == NW * TPW)
+          bwd(std::true_type{}, std::true_type{});
+        else
+          bwd(std::true_type{}, std::false_type{});
+      } else {
+        bwd(std::false_type{}, std::false_type{});
+      }
+      if (ilv) {
+        if (w == 0 && lg == 0)                     // (after the rows: nothing waits on it here)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) lb[rt] = P.labels[pn[rt]];
+        lc_ok = sp_advance(lc, P, grp, ng, T);
+        if (lc_ok) fetch_rows();
       }
       npn = wave_sum_dpp(npn, lane);
       nwn = wave_sum_dpp(nwn, lane);
@@ -639,20 +670,27 @@ static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t
   hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED, NW>), dim3(grid), dim3(NW * 64), lds, st, P, X);
 }
 
-// default: 1 where half the waves streaming during the hand-off pays (parallel clients, G <= 8:
-// config 2 24.2k vs 25.7k cycles per step); 0 for chained clients (32 KB per CU per step:
-// config 1 at G = 8 13.8k vs 14.8k), G = 16 and 4-wave workgroups
+// default: 2 for 8-wave workgroups -- r02q, us per launch, schedules 0 / 1 / 2 / 3: config 2
+// (G = 2) 365 / 367 / 353 / 357; config 4 (G = 2) 513 / 503 / 483 / 501; config 3 (G = 4) 5085 /
+// 5169 / 4860 / 5162; config 5 (G = 16) 6692 / - / 6187 / -; chained config 1 (G = 8) 9066 /
+// 9576 / 8456 / 8391.  4-wave workgroups (opt-in) keep 0.
 static int split_sched(int G, int NW, bool chained) {
+  (void)G;
+  (void)chained;
   const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
-  if (s) return std::max(0, std::min(1, atoi(s)));
-  return (chained || G >= 16 || NW == 4) ? 0 : 1;  // (4-wave hand-off threads: all of them)
+  if (s) return std::max(0, std::min(3, atoi(s)));
+  return NW == 4 ? 0 : 2;
 }
 
 template <int RT, int G, bool PROX>
 static void launch_split_p(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
   const int sc = split_sched(G, NW, P.chained != 0);
-  if constexpr (G >= 16) {
+  if (NW == 8 && sc == 2) {
+    launch_split_s<RT, G, PROX, 2, 8>(P, X, grid, lds, st);
+  } else if constexpr (G >= 16) {
     launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);     // the hand-off values need all 512 threads
+  } else if (NW == 8 && sc == 3) {
+    launch_split_s<RT, G, PROX, 3, 8>(P, X, grid, lds, st);
   } else {
     if (NW == 4) {
       if (sc == 0) launch_split_s<RT, G, PROX, 0, 4>(P, X, grid, lds, st);

@@ -194,6 +194,33 @@ def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
             start = Wr
 
 
+@pytest.mark.parametrize('sched', [0, 1, 2, 3])
+@pytest.mark.parametrize('G,D', [(2, 2048), (4, 1000), (16, 4096)])
+@pytest.mark.parametrize('chained', [False, True])
+def test_local_train_split_schedules(amd, monkeypatch, sched, G, D, chained):
+    """Every hand-off / row-streaming schedule of the group kernel (FS_SP_SCHED; 2 is the
+    default: each wave's next rows are interleaved into its backward) against the oracle, with
+    full slices (16 tiles per workgroup: the straight-line interleaved backward) and ragged
+    ones (D = 1000), FedProx + ridge, chained and parallel."""
+    monkeypatch.setenv('FS_SP_SCHED', str(sched))
+    rs = np.random.RandomState(sched + 10 * G + chained)
+    C, B, E = 7, 32, 2
+    sizes = [70, 0, 33, 64, 9]
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    lr, mu, lam = 0.4, 0.03, 0.002
+    W, loss = _train_via_abi(amd, Xs, ys, W0, lr, E, B, True, mu, True, lam, chained, seed=5, split=G)
+    assert _train_via_abi.last_G == G
+    torch.manual_seed(5)
+    start = W0
+    for j, (X, y) in enumerate(zip(Xs, ys)):
+        Wr, lref = O.train_client(X, y, start, lr, E, B, True, mu, True, lam)
+        assert np.abs(W[j] - Wr).max() <= 2e-5 * max(1.0, np.abs(Wr).max()), (j, np.abs(W[j] - Wr).max())
+        assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
+        if chained:
+            start = Wr
+
+
 @pytest.mark.parametrize('N,G', [(300, 2), (700, 4)])
 def test_local_train_persistent_groups(amd, N, G):
     """More clients than groups (N * G > CUs): every group walks several clients in the
