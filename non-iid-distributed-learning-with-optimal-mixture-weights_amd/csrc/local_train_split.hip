@@ -184,7 +184,12 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---- weights (and prox anchor) of this slice into registers: the round-start model ----
-  float4 wr[TPW][4], ar[TPW][4];
+  float4 wr[TPW][4];
+  // the prox anchor (the client's start) is not kept in registers -- 32 more VGPRs per lane
+  // spilled every prox variant -- but re-read in the update: W_start (parallel clients: one
+  // [C][ld] model shared by every group, L2-resident) or the previous chained client's result,
+  // which this workgroup itself stored at that client's end
+  const float* anc = P.W_start;
   // (the weight addresses are rebuilt behind an empty asm at every use: they are used only at
   // client boundaries and must not be hoisted into registers that live across the step loop)
   auto wbase = [&]() {
@@ -307,12 +312,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       } else if (lane == 0) {
         wred[w][0] = 0.f;                         // ||W - W_a|| = 0 at the new anchor
       }
-      if (PROX) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ar[i][q] = wr[i][q];
-      }
+      if (PROX) anc = (P.chained && cc.j > 0) ? P.W_out + (int64_t)(cc.j - 1) * C * ld : start;
       lsum = 0.0;
     }
     {
@@ -523,6 +523,12 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       for (int i = 0; i < TPW; ++i) {
         const int Tl = w + NW * i;
         if (decltype(FULL)::value || Tl < NTS) {
+          float4 av[4];                            // prox anchor of this tile (issued first: the
+          if (PROX && l16 < C) {                   // update waits only for these, not the rows)
+            const float* ap = anc + wbase() + 64 * Tl;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[q] = ld4(ap + 16 * q);
+          }
           floatx4 ga[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) ga[e4] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -541,7 +547,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
 #pragma unroll
               for (int e4 = 0; e4 < 4; ++e4) {
                 const float wc = comp(wr[i][q], e4);
-                const float ac = PROX ? comp(ar[i][q], e4) : 0.f;
+                const float ac = PROX ? comp(av[q], e4) : 0.f;
                 float gr = ga[e4][q];
                 if (PROX) gr = gr + (wc - ac) * sp;
                 if (P.reg) gr = gr + wc * sr;
@@ -755,7 +761,7 @@ using namespace fs;
 // workspace bytes it needs.  On entry *G_out is a request: 0 = let the planner choose,
 // 1 = one workgroup per client, 2..16 = that group width if the shape allows it (else the
 // planner's choice).  FS_SPLIT_G in the environment overrides a 0 request (diagnostics).
-// prox: the FedProx term is on (its split variants carry the anchor in registers).
+// prox: the FedProx term is on (kept in the ABI; every split variant covers it).
 // max_en = max_j E * n_j.
 extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                                    int* G_out, int64_t* ws_bytes_out) {
@@ -780,13 +786,13 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
           if (bytes / cand <= 32 * 1024) break;
         }
     } else {
-      // parallel clients: the narrowest group that fits (most clients in flight, fewest partners).
-      // The prox variants hold the anchor slice in registers too and spill at 256 VGPRs; with
-      // enough clients to fill the chip one workgroup per client is as fast, so they split
-      // only when that leaves most CUs idle.
+      // parallel clients: the narrowest group that fits (most clients in flight, fewest
+      // partners) -- FedProx too since its anchor is re-read, not register-resident (r02t, prox,
+      // us per launch, G = 1 vs split: config 2 741 / 362, config 3 5955 / 5263, config 4
+      // 580 / 508, config 5 11237 / 7003)
       for (int cand : {2, 4, 8, 16})
         if (split_fits(C, B, NT, cand) && cand <= cus) { G = cand; break; }
-      if (prox && G > 0 && 2 * N >= cus) G = 0;
+      (void)prox;
     }
   }
   (void)max_en;
