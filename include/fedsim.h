@@ -149,7 +149,7 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * otherwise one LDS-staged / global workgroup.
  * d_ws: fs_mix_solve_ws_bytes(N, C, Bv) bytes, zeroed once at allocation (the multi-CU
  * exchange granules + the error block; a timed-out exchange also writes NaN into d_p).
- * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=reg2|reg|mc|staged|global
+ * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=wave|reg2|reg|mc|staged|global
  * forces one solver (FS_MIX_SWAP=0: reg2 without the permlane swap-add levels).
  * ------------------------------------------------------------------------- */
 int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv);
@@ -159,7 +159,8 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
 
 /* Diagnostic (host state only): the solver the calling thread's last fs_mix_solve
  * launched -- 1 register-resident (one row per wave), 2 multi-CU, 3 LDS-staged, 4 global,
- * 5 register-resident form 2 (two rows per wave, Bv <= 16, C <= 10); 0 = none yet. */
+ * 5 register-resident form 2 (two rows per wave, Bv <= 16, C <= 10), 6 one wave (N <= 16,
+ * C <= 4, Bv <= 16); 0 = none yet. */
 int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *

@@ -801,6 +801,126 @@ static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, con
 }
 
 // ----------------------------------------------------------------------------
+// p-solve, one wave (N <= 16, C <= 4, Bv <= 16: config 1's FedAMW, N = 10, C = 2).  At this
+// size a step moves 16 x C x N floats; the workgroup solvers' fixed per-step cost (a barrier,
+// LDS partial sums, one batch row per wave) is the whole of their ~1 us.  Here one wave holds
+// the step: lane l = (row b = l / 4, class c = l % 4) holds its Z segment (16 clients, 4 float4);
+// the logit is a 16-term dot product with p held in SGPRs; the softmax runs over the row's 4
+// lanes (DPP); the gradient g_{b,c} * Z segment is reduce-scattered over the wave so that lanes
+// 4n .. 4n+3 hold client n's total (lanes.h class_totals), which they use to step p_n and the
+// momentum buffer; 16 readlanes return p to SGPRs.  No barrier, no LDS.  The next DEPTH steps'
+// rows stream in behind (Z segments and labels, their row indices DEPTH steps earlier still).
+// ----------------------------------------------------------------------------
+constexpr int MW_DEPTH = 6;
+
+__global__ __launch_bounds__(64) void mix_solve_wave_kernel(const float* __restrict__ Z,
+                                                           const int32_t* __restrict__ y,
+                                                           const int32_t* __restrict__ perms, int N, int C, int nv,
+                                                           int epochs, int Bv, float lr, float mom,
+                                                           float* __restrict__ p, float* __restrict__ buf,
+                                                           int* __restrict__ first_flag) {
+  const int lane = threadIdx.x;
+  const int b = lane >> 2, c = lane & 3;
+  const int ldN = mix_ldn(N);                      // <= 16
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int cc = min(c, C - 1);
+  int coff[4];                                     // this lane's four float4 of its class segment
+#pragma unroll
+  for (int k = 0; k < 4; ++k) coff[k] = cc * ldN + min(4 * k, ldN - 4);   // (past ldN: p = 0 there)
+  const int mn = lane >> 2;                        // the client this lane steps after the reduce-scatter
+  float pr = mn < N ? p[mn] : 0.f;
+  float br = mn < N ? buf[mn] : 0.f;
+  float sp[16];
+#pragma unroll
+  for (int n = 0; n < 16; ++n)
+    sp[n] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pr), 4 * n));
+  int first = *first_flag;
+  // row index of the next step in fetch order (this lane's row; rows past the batch read its
+  // first row, their gradient is 0); the cursor stays on the last step at the end
+  int fst = 0, fep = 0, fsb = 0;
+  auto next_row = [&]() -> int {
+    const int bc = min(Bv, nv - fsb * Bv);
+    const int r = perms[(int64_t)fep * nv + fsb * Bv + (b < bc ? b : 0)];
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+    return r;
+  };
+  float4 zr[MW_DEPTH][4];
+  int lab[MW_DEPTH], idx[MW_DEPTH];
+#define MW_ISSUE(R_, ROW_)                                                                 \
+  {                                                                                        \
+    const float* zp_ = Z + (int64_t)(ROW_) * CN;                                           \
+    _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) zr[R_][q_] = ld4(zp_ + coff[q_]);    \
+    lab[R_] = y[(ROW_)];                                                                   \
+  }
+#pragma unroll
+  for (int r0 = 0; r0 < MW_DEPTH; ++r0) {          // steps 0 .. DEPTH-1: rows in flight
+    const int r = next_row();
+    MW_ISSUE(r0, r);
+  }
+#pragma unroll
+  for (int r0 = 0; r0 < MW_DEPTH; ++r0) idx[r0] = next_row();   // steps DEPTH .. 2 DEPTH-1
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): the loop inherits only its own order
+  int s = 0, csb = 0;
+#define MW_STEP(R_)                                                                        \
+  {                                                                                        \
+    if (s >= total) break;                                                                 \
+    const int bc = min(Bv, nv - csb * Bv);                                                 \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                   \
+    float o0 = 0.f, o1 = 0.f;                                                              \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                        \
+      o0 += zr[R_][k].x * sp[4 * k + 0];                                                   \
+      o1 += zr[R_][k].y * sp[4 * k + 1];                                                   \
+      o0 += zr[R_][k].z * sp[4 * k + 2];                                                   \
+      o1 += zr[R_][k].w * sp[4 * k + 3];                                                   \
+    }                                                                                      \
+    const float o = o0 + o1;                                                               \
+    const bool real = c < C;                                                               \
+    float m = real ? o : -INFINITY;                                                        \
+    m = fmaxf(m, xor_get(m, 1, lane));                                                     \
+    m = fmaxf(m, xor_get(m, 2, lane));                                                     \
+    float e = real ? expf(o - m) : 0.f;                                                    \
+    e += xor_get(e, 1, lane);                                                              \
+    e += xor_get(e, 2, lane);                                                              \
+    const float invb = 1.0f / (float)bc;                                                   \
+    const float g = (real && b < bc) ? (c == lab[R_] ? -invb : 0.f) + expf(o - m - logf(e)) * invb : 0.f; \
+    float v[16];                                                                           \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                        \
+      v[4 * k + 0] = g * zr[R_][k].x;                                                      \
+      v[4 * k + 1] = g * zr[R_][k].y;                                                      \
+      v[4 * k + 2] = g * zr[R_][k].z;                                                      \
+      v[4 * k + 3] = g * zr[R_][k].w;                                                      \
+    }                                                                                      \
+    const float gp = class_totals<16>(v, lane);                                            \
+    /* the slot is consumed: refill it with step s + DEPTH, fetch the rows of s + 2 DEPTH */ \
+    MW_ISSUE(R_, idx[R_]);                                                                 \
+    idx[R_] = next_row();                          /* step s + 2 DEPTH */                  \
+    if (mn < N) momentum_step(pr, br, gp, first, mom, lr);                                 \
+    first = 0;                                                                             \
+    _Pragma("unroll") for (int n = 0; n < 16; ++n)                                         \
+      sp[n] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pr), 4 * n)); \
+    ++s;                                                                                   \
+  }
+  for (;;) {
+    MW_STEP(0) MW_STEP(1) MW_STEP(2) MW_STEP(3) MW_STEP(4) MW_STEP(5)
+  }
+#undef MW_STEP
+#undef MW_ISSUE
+  if ((lane & 3) == 0 && mn < N) {
+    p[mn] = pr;
+    buf[mn] = br;
+  }
+  if (lane == 0 && total > 0) *first_flag = 0;
+}
+
+// ----------------------------------------------------------------------------
 // p-solve, multi-CU form (Bv <= 16, C <= 16, N <= 2048).  One workgroup on one CU cannot
 // stream a batch of Z rows faster than ~33 GB/s (gathered rows from the Infinity Cache,
 // MI355X_MICROARCH.md "Indexed rows"): at config 2 that is 64 KB per step, ~2 us -- the
@@ -1157,6 +1277,13 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // auto: the single-CU register solver where an instance covers the shape (no cross-CU
   // exchange: ~1-2.5 us per step), else the multi-CU solver (~4-7 us per step, 7-11x the
   // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
+  if (((want == "auto" && N <= 16 && C <= 4 && Bv <= 16) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
+    hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
+                       Bv, lr_p, momentum, d_p, d_buf, d_first);
+    t_last_solver = 6;
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
   // form 2 (two rows per wave) where it measured faster: N in (128, 256], NK = 4 (2.0 vs 4.1 us
   // per step at N = 256, C = 4); below that the one-row form is as fast or faster (r02g)
   if (((want == "auto" && N > 128) || want == "reg2") &&

@@ -301,7 +301,10 @@ def test_eval_unit_golden(amd):
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [
-    (10, 2, 203, 16),       # config 1 shape: register solver form 2, NK=1, CP=2
+    (10, 2, 203, 16),       # config 1 shape: one-wave solver
+    (16, 4, 77, 16),        # one wave, every lane's class real, ragged last batch
+    (5, 3, 40, 7),          # one wave, Bv < 16 (idle rows), N not a multiple of 4
+    (1, 2, 33, 16),         # one client
     (100, 10, 517, 16),     # config 2 shape: NK=2, CP=16 (10 loaded classes)
     (200, 4, 301, 16),      # NK=4, CP=4 (at lr 0.1: lr 0.5 makes this p-SGD ill-conditioned, fp32 vs fp64 2e-4)
     (60, 8, 33, 9),         # CP=8, 9-row batches: the second row of every wave idles
@@ -338,6 +341,26 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         ep = float(np.abs(mix.p.cpu().numpy() - pr).max() / np.abs(pr).max())
         eb = float(np.abs(mix.buf.cpu().numpy() - br).max() / np.abs(br).max())
         assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
+
+
+@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'wave'), (16, 4, 16, 'wave'), (17, 4, 16, 'reg'),
+                                           (10, 5, 16, 'reg'), (100, 10, 16, 'reg'), (200, 4, 16, 'reg2'),
+                                           (1000, 10, 16, 'mc'), (23, 5, 24, 'staged')])
+def test_mix_solve_auto_choice(amd, N, C, Bv, solver):
+    """The solver fs_mix_solve picks by shape."""
+    rs = np.random.RandomState(N)
+    nv, D = 40, 64
+    Xv = (np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=nv).astype(np.int64)
+    p0 = np.full(N, 1.0 / N, np.float32)
+    dev = torch.device('cuda')
+    mix = amd.engine.Mixture(torch.from_numpy(Xv), torch.from_numpy(yv), D, C, N, Bv, torch.from_numpy(p0), dev)
+    Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+    torch.manual_seed(0)
+    mix.solve(Wd, amd.rng.draw_pass_seeds(1), 0.1)
+    torch.cuda.synchronize()
+    mix.check_errors()
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
 
 
 @pytest.mark.parametrize('hops', [1, 2])
