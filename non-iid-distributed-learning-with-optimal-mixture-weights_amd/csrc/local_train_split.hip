@@ -131,7 +131,9 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 //   2  every wave runs the hand-off; no wave issues its next rows in a burst: each issues
 //      one row load per backward iteration (16 per wave per step), so the issue stalls of a
 //      full memory queue land between the backward's MFMAs instead of ahead of them.
-//   3  as 1 for the second half; the first half interleaves its rows into the backward as 2.
+// (Tried and dropped, r02q / r02w: the first half interleaving as 2 while the second half
+// streams during the hand-off as 1 -- no faster; 2 plus the first 4 or 8 row loads of each
+// wave issued right after its image write -- slower at every BASELINE shape.)
 template <int RT, int G, bool PROX, int SCHED, int NWV>
 __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_kernel(LTParams P, SplitWS X) {
   constexpr int NW = NWV;
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
-  constexpr int XT = (SCHED == 1 || SCHED == 3) ? NTH / 2 : NTH;   // threads running the hand-off
+  constexpr int XT = SCHED == 1 ? NTH / 2 : NTH;  // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
   constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
   constexpr int HC = G;                             // partners polled per round trip
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
 
-      const bool xw = SCHED == 0 || SCHED == 2 || w < NW / 2;   // this wave runs the hand-off
+      const bool xw = SCHED != 1 || w < NW / 2;      // this wave runs the hand-off
       if (!xw) {
         SP_IMG_WRITE();
         SP_NEXT();
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       const int rblk = 4 * (l16 & 3) + (l16 >> 2);
       float npn = 0.f, nwn = 0.f;
       // schedules 2 / 3: this wave's next rows go out one load per backward iteration
-      const bool ilv = lc_ok && (SCHED == 2 || (SCHED == 3 && w < NW / 2));
+      const bool ilv = lc_ok && SCHED == 2;
       // (two instances, so the interleaved loads are straight-line code: a branch around each
       // load would make the compiler wait for it at the join)
       // FULL: every wave owns TPW tiles (NTS = NW * TPW, every BASELINE shape but chained config
@@ -676,15 +678,15 @@ static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t
   hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED, NW>), dim3(grid), dim3(NW * 64), lds, st, P, X);
 }
 
-// default: 2 for 8-wave workgroups -- r02q, us per launch, schedules 0 / 1 / 2 / 3: config 2
-// (G = 2) 365 / 367 / 353 / 357; config 4 (G = 2) 513 / 503 / 483 / 501; config 3 (G = 4) 5085 /
-// 5169 / 4860 / 5162; config 5 (G = 16) 6692 / - / 6187 / -; chained config 1 (G = 8) 9066 /
-// 9576 / 8456 / 8391.  4-wave workgroups (opt-in) keep 0.
+// default: 2 for 8-wave workgroups -- r02q, us per launch, schedules 0 / 1 / 2: config 2
+// (G = 2) 365 / 367 / 353; config 4 (G = 2) 513 / 503 / 483; config 3 (G = 4) 5085 / 5169 /
+// 4860; config 5 (G = 16) 6692 / - / 6187; chained config 1 (G = 8) 9066 / 9576 / 8456.
+// 4-wave workgroups (opt-in) keep 0.
 static int split_sched(int G, int NW, bool chained) {
   (void)G;
   (void)chained;
   const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
-  if (s) return std::max(0, std::min(3, atoi(s)));
+  if (s) return std::max(0, std::min(2, atoi(s)));
   return NW == 4 ? 0 : 2;
 }
 
@@ -695,8 +697,6 @@ static void launch_split_p(const LTParams& P, const SplitWS& X, int NW, int grid
     launch_split_s<RT, G, PROX, 2, 8>(P, X, grid, lds, st);
   } else if constexpr (G >= 16) {
     launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);     // the hand-off values need all 512 threads
-  } else if (NW == 8 && sc == 3) {
-    launch_split_s<RT, G, PROX, 3, 8>(P, X, grid, lds, st);
   } else {
     if (NW == 4) {
       if (sc == 0) launch_split_s<RT, G, PROX, 0, 4>(P, X, grid, lds, st);

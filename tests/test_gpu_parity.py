@@ -194,7 +194,7 @@ def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
             start = Wr
 
 
-@pytest.mark.parametrize('sched', [0, 1, 2, 3])
+@pytest.mark.parametrize('sched', [0, 1, 2])
 @pytest.mark.parametrize('G,D', [(2, 2048), (4, 1000), (16, 4096)])
 @pytest.mark.parametrize('chained', [False, True])
 def test_local_train_split_schedules(amd, monkeypatch, sched, G, D, chained):
