@@ -1,0 +1,7 @@
+#!/bin/bash
+# PMC traffic of the final group kernel at configs 2, 4, 3 (five counter passes each)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+bash scripts/pmc_capture.sh c2 "--config 2 --steps 3 --warmup 1 --no-fedamw-leg" "local_train" || exit 1
+bash scripts/pmc_capture.sh c4 "--config 4 --steps 3 --warmup 1" "local_train" || exit 1
+bash scripts/pmc_capture.sh c3 "--config 3 --steps 2 --warmup 1" "local_train" || exit 1
