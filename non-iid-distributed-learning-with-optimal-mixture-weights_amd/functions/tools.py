@@ -30,6 +30,8 @@ All arithmetic of the round runs in the gfx950 kernels of libfedsim.so; there is
 CPU path.  ``type`` must be 'classification' (the reference's MSE branch,
 tools.py:183-184, is not on the benchmarked path).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -224,15 +226,25 @@ class Federation:
             return out
 
         timed('train', lambda: self.plan.round(t, self.lr, P[0]))
+        early = False
         if self.mixture is not None:
             self._train_done = torch.cuda.Event()
             self._train_done.record()
+            # FedAMW: round t+1's shuffles are enqueued now (nothing else draws from the global
+            # generator in between, so the draw order is unchanged) and the p-solve waits for the
+            # validation shuffles: they run beside the Z GEMM, not on the CUs of the p-solve's
+            # workgroups (FS_FEDAMW_SHUFFLE=late: after the round, beside the p-solve)
+            early = self.t + 1 < self.R and os.environ.get('FS_FEDAMW_SHUFFLE', 'early') != 'late'
+            if early:
+                self._prepare(t + 1)
         if self.zshard:
             # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
             self.p_hist[t].copy_(self.mixture.p[self.pos_dev])
             timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local))
             timed('z_allgather', lambda: dist.allgather_z(self.Z_local, self.C, self.mixture.Z))
+            if early:
+                torch.cuda.current_stream().wait_stream(self.side)
             p = timed('solve', lambda: self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False))
             self.agg.run(self.trainer.W_out, self.p_slice(p), self.W_g)
             dist.allreduce_sum_(self.W_g)
@@ -240,6 +252,8 @@ class Federation:
         elif self.mixture is not None:
             self.p_hist[t].copy_(self.mixture.p)
             timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.N, self.mixture.Z))
+            if early:
+                torch.cuda.current_stream().wait_stream(self.side)
             p = timed('solve', lambda: self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False))
             self.agg.run(self.trainer.W_out, p, self.W_g)
             self.plan.round(t, self.lr, P[2])
@@ -252,7 +266,7 @@ class Federation:
         if self.W_hist is not None:
             self.W_hist[t].copy_(self.W_g)
         self.t += 1
-        if self.t < self.R:
+        if self.t < self.R and not early:
             self._prepare(self.t)
 
     def results(self):
