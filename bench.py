@@ -199,11 +199,17 @@ def main():
     args = parse()
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    # (ranks wrap onto the visible devices and FS_BENCH_BACKEND=gloo swaps RCCL out: only to
+    # rehearse the multi-rank path on a one-GPU box; the driver's runs are one rank per GPU)
+    local = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if ws > 1:
-        tdist.init_process_group('nccl', device_id=dev)
+        backend = os.environ.get('FS_BENCH_BACKEND', 'nccl')
+        if backend == 'nccl':
+            tdist.init_process_group('nccl', device_id=dev)
+        else:
+            tdist.init_process_group(backend)
     strong = args.config in STRONG and not args.custom
     N_loc = args.clients // ws if strong else args.clients
     if N_loc < 1:
@@ -222,7 +228,7 @@ def main():
     N_all = N_loc * ws
     shards = fdist.shard_lpt(fdist.client_work(np.full(N_all, args.rows), E, B), ws)
     Xs = [None] * N_all
-    ys = [torch.empty(args.rows, dtype=torch.int64)] * N_all
+    ys = [torch.zeros(args.rows, dtype=torch.int64)] * N_all      # other ranks' clients: lengths only
     for k, j in enumerate(shards[rank]):
         Xs[j], ys[j] = d['X_train'][k], d['y_train'][k]
     lr, mu = 0.5, (5e-4 if args.algo == 'fedprox' else 0.0)

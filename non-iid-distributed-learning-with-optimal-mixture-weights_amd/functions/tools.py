@@ -77,7 +77,8 @@ def _check_labels(ys, num_classes, what):
                                                                               int(y.max())))
 
 
-def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test=None, y_val=None):
+def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test=None, y_val=None,
+                  train_labels=True):
     if type != 'classification':
         raise NotImplementedError("only type='classification' is implemented (tools.py:181-184 MSE branch "
                                   "is out of scope)")
@@ -93,7 +94,8 @@ def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round,
         raise NotImplementedError('batch_size must be in [1, 64]')
     if epoch < 1 or round < 0:
         raise ValueError('epoch must be >= 1 and round >= 0')
-    _check_labels(y_train, num_classes, 'training')
+    if train_labels:
+        _check_labels(y_train, num_classes, 'training')
     if y_test is not None:
         _check_labels([y_test], num_classes, 'test')
     if y_val is not None:
@@ -107,8 +109,10 @@ class Federation:
     def __init__(self, algo, X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
                  batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=None, verbose=True,
                  shuffle_device=True):
+        # (training labels: only this rank's clients, below -- in sharded mode the other ranks'
+        # entries of X_train / y_train need only have the right lengths)
         _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test,
-                      validloader.dataset.tensors[1] if validloader is not None else None)
+                      validloader.dataset.tensors[1] if validloader is not None else None, train_labels=False)
         if clients not in ('sequential', 'parallel'):
             raise ValueError("clients must be 'sequential' or 'parallel'")
         self.chained = clients == 'sequential'
@@ -117,7 +121,6 @@ class Federation:
         if self.sharded and len(y_train) < nranks:
             raise ValueError("clients='parallel' over %d ranks needs at least one client per rank (got %d clients)"
                              % (nranks, len(y_train)))
-        dev = _device()
         self.algo, self.stats, self.verbose = algo, stats, verbose
         self.C, self.E, self.B, self.R, self.D = int(num_classes), int(epoch), int(batch_size), int(round), int(D)
         self.lr, self.lr_p, self.prox, self.mu, self.reg, self.lam = lr, lr_p, prox, mu, lambda_reg_if, lambda_reg
@@ -129,6 +132,8 @@ class Federation:
         self.shards = dist.shard_lpt(dist.client_work(ns, E, B), nranks) if self.sharded else [np.arange(N)]
         self.mine = self.shards[self.rank] if self.sharded else self.shards[0]
         mine = self.mine
+        _check_labels([y_train[j] for j in mine], num_classes, 'training')
+        dev = _device()
 
         # model init + mixture weights exactly as the reference (tools.py:330-333, 414-417)
         W_init = init_weights(D, C)

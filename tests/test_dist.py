@@ -157,3 +157,49 @@ def test_parallel_clients_need_one_per_rank():
     mp.spawn(_rank_check_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
         assert 'at least one client per rank' in out[r], out[r]
+
+
+def _label_shard_worker(rank, world, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import fedamw_amd  # noqa: F401
+        from fedamw_amd import dist as fdist
+        from fedamw_amd.functions import tools
+        ns = np.array([5, 7, 6, 9])
+        mine = fdist.shard_lpt(fdist.client_work(ns, 1, 32), world)[rank]
+        res = []
+        for bad_own in (False, True):
+            # the other rank's clients carry garbage labels (bench.py passes placeholders there)
+            y = [torch.full((int(n),), 999, dtype=torch.int64) for n in ns]
+            for j in mine:
+                y[j] = torch.zeros(int(ns[j]), dtype=torch.int64)
+            if bad_own:
+                y[mine[0]][0] = 5
+            X = [torch.zeros(int(n), 8) for n in ns]
+            try:
+                tools.FedAvg(X, y, X[0], y[0][:1] * 0, 'classification', 2, 8, 0.1, 1, 32, False, 0.0, False, 0.0, 1,
+                             clients='parallel', verbose=False)
+                res.append('no error')
+            except ValueError as e:
+                res.append('ValueError: ' + str(e))
+            except RuntimeError as e:          # no GPU here: past every input check
+                res.append('RuntimeError')
+        out[rank] = res
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_sharded_label_check_covers_own_clients_only():
+    """clients='parallel' under torch.distributed: each rank validates the labels of ITS clients
+    only -- the other ranks' entries need only have the right lengths (bench.py's placeholders)
+    -- and an out-of-range label among its own clients is still a ValueError."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_label_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        ok, bad = out[r]
+        assert 'labels must lie' not in ok, ok
+        assert bad.startswith('ValueError') and 'training labels' in bad, bad
