@@ -120,15 +120,14 @@ def stream_ptr(stream=None):
 
 
 def source_revision():
-    """sha256 (16 hex digits) of every kernel / C-ABI source of libfedsim.so (csrc/ and
-    include/fedsim.h).  Profiles under profiles/ record it; bench.py uses a PMC traffic
+    """sha256 (16 hex digits) of the device sources of libfedsim.so -- the kernels and the
+    headers they include (csrc/*.hip, csrc/*.h; host-only .cpp files and the C-ABI header
+    carry no device code).  Profiles under profiles/ record it; bench.py uses a PMC traffic
     figure only when it was measured on kernels with this exact revision."""
     import hashlib
     import glob
     pkg = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(pkg, 'csrc', '*.hip')) + glob.glob(os.path.join(pkg, 'csrc', '*.h'))
-                   + glob.glob(os.path.join(pkg, 'csrc', '*.cpp')))
-    files.append(os.path.join(os.path.dirname(pkg), 'include', 'fedsim.h'))
+    files = sorted(glob.glob(os.path.join(pkg, 'csrc', '*.hip')) + glob.glob(os.path.join(pkg, 'csrc', '*.h')))
     h = hashlib.sha256()
     for f in files:
         h.update(os.path.basename(f).encode())
