@@ -59,6 +59,22 @@ int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, const int64_t*
                       int64_t npasses, int32_t* h_out, int nthreads);
 
 /* ------------------------------------------------------------------------- *
+ * Host: LIBSVM / svmlight reader.  Replaces the parse of svmlight_data
+ * (utils.py:36-38, sklearn load_svmlight_file) for the dense float32 rows
+ * load_full_data feeds the feature map (utils.py:56): `label [qid:q] idx:val ...`
+ * per line, `#` comments, blank lines skipped; values parsed as doubles and rounded
+ * once to float32 (= csr.toarray().astype(float32)).  fs_libsvm_scan reports the
+ * sample count and the smallest / largest feature index (-1: no features).
+ * fs_libsvm_read fills X [n_rows][n_features] (zeroed first) and y [n_rows];
+ * zero_based: 1 indices start at 0, 0 at 1, -1 auto (zero-based iff the smallest
+ * index is 0, as sklearn's 'auto'); an index outside n_features is an error.
+ * Parallel over line-aligned chunks (nthreads <= 0: min(16, hardware)).
+ * ------------------------------------------------------------------------- */
+int fs_libsvm_scan(const char* path, int64_t* n_rows, int64_t* min_index, int64_t* max_index);
+int fs_libsvm_read(const char* path, int64_t n_rows, int64_t n_features, int zero_based, float* X, double* y,
+                   int nthreads);
+
+/* ------------------------------------------------------------------------- *
  * Device: the same shuffle replay as fs_randperm_batch, on the GPU (one wave per
  * pass; d_seeds/d_n/d_off are device arrays of npasses int64; max_n bounds n[i] and
  * selects an LDS-resident (max_n <= ~38K) or in-place global-memory permutation).

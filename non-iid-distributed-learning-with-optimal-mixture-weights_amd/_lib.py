@@ -17,6 +17,8 @@ _SIGS = {
     'fs_abi_version': (C.c_int, []),
     'fs_last_error': (C.c_char_p, []),
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
+    'fs_libsvm_scan': (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    'fs_libsvm_read': (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
     'fs_randperm_device': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                      C.c_void_p]),
     'fs_local_train_plan': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int,

@@ -9,18 +9,22 @@ Differences from the reference, all deliberate and stated:
   * the reference returns full-batch DataLoaders whose ``.next()`` exp.py:61-62 calls
     (gone in torch 2); ``load_full_data`` here returns the dense arrays and the driver
     replays the two loaders' RNG use itself (``full_batch_order``);
-  * LIBSVM files are parsed with scikit-learn's ``load_svmlight_file`` (what the
-    reference uses, utils.py:38); the test file is read with the training file's width
-    (a9a.t is one column narrower than a9a -- SURVEY Q14 -- which breaks the reference's
-    matmul);
+  * LIBSVM files are parsed by the native reader ``fs_libsvm_scan`` / ``fs_libsvm_read``
+    (csrc/libsvm.cpp: multi-threaded, the rules of scikit-learn's ``load_svmlight_file``,
+    which the reference calls at utils.py:38, and the same float32 values --
+    tests/test_libsvm.py checks it against sklearn); the test file is read with the training
+    file's width (a9a.t is one column narrower than a9a -- SURVEY Q14 -- which breaks the
+    reference's matmul);
   * when the LIBSVM file is absent (no datasets ship with the reference or this image),
     ``load_full_data`` synthesises a dataset of the same shape from a private generator
     (``synthetic_libsvm``), so the global numpy / torch streams are consumed exactly as
     a file load consumes them (not at all).
 The partitioner is a restatement of the reference's numpy algorithm (same calls, same
-order, on the global numpy generator reseeded to 2020 as utils.py:320 does); the
-reference's ``utils.py`` cannot be imported here (top-level torchvision import, absent),
-so its bit-compatibility is checked by properties, not against reference output.
+order, on the global numpy generator reseeded to 2020 as utils.py:320 does -- it stays on
+numpy because its draws ARE numpy's legacy generator), pinned to the reference's own output:
+tests/golden/make_golden.py imports the reference's utils.py behind an in-process
+torchvision stub and records get_Dirichlet_distribution and the whole exp.py:60-99 data
+path (tests/test_oracle_prep.py).
 """
 import os
 
@@ -37,6 +41,26 @@ SYNTH_SHAPES = {
     'a9a': (32561, 16281, 123, 2, 'a9a'),
     'covtype': (464810, 116202, 54, 7, 'covtype'),
 }
+
+
+def read_libsvm(path, n_features=None, zero_based=-1, nthreads=0):
+    """A LIBSVM / svmlight file as dense float32 rows + float64 labels (the native reader,
+    csrc/libsvm.cpp; the values of ``load_svmlight_file(path)[0].toarray().astype(float32)``).
+    ``zero_based``: -1 auto (zero-based iff the smallest index is 0), 0 or 1.  Returns
+    (X, y, zero_based_used, n_features)."""
+    import ctypes
+    from .. import _lib
+    L = _lib.lib()
+    bpath = os.fsencode(path)
+    n, mn, mx = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(L.fs_libsvm_scan(bpath, ctypes.byref(n), ctypes.byref(mn), ctypes.byref(mx)), 'fs_libsvm_scan')
+    zb = zero_based if zero_based in (0, 1) else (1 if mn.value == 0 else 0)
+    d = int(n_features) if n_features is not None else max(0, mx.value + (1 if zb else 0))
+    X = np.empty((n.value, d), np.float32)
+    y = np.empty(n.value, np.float64)
+    _lib.check(L.fs_libsvm_read(bpath, n.value, d, zb, X.ctypes.data, y.ctypes.data, int(nthreads)),
+               'fs_libsvm_read')
+    return X, y, zb, d
 
 
 def svmlight_labels(y, dataset):
@@ -128,10 +152,8 @@ def load_full_data(dataset_name, num_partitions=10, alpha=0.1, root_dir='../FedA
     dataset's full shape)."""
     path = os.path.join(root_dir, dataset_name)
     if os.path.exists(path):
-        from sklearn.datasets import load_svmlight_file
-        Xs, y = load_svmlight_file(path)
-        Xts, yt = load_svmlight_file(path + '.t', n_features=Xs.shape[1])
-        X, Xt = Xs.toarray().astype(np.float32), Xts.toarray().astype(np.float32)
+        X, y, zb, d = read_libsvm(path)
+        Xt, yt, _, _ = read_libsvm(path + '.t', n_features=d, zero_based=zb)
         y, yt = svmlight_labels(y, dataset_name), svmlight_labels(yt, dataset_name)
     else:
         X, y, Xt, yt = synthetic_libsvm(dataset_name, **(synth or {}))
