@@ -547,6 +547,295 @@ static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, cons
 }
 
 // ----------------------------------------------------------------------------
+// p-solve, row-split form (Bv <= 16, N <= 64*NK, C <= CL): the register solver's layout on
+// K = 16/RW workgroups, workgroup k owning batch rows k*RW .. k*RW+RW-1 of every step.  A
+// workgroup has its rows' full Z rows, so it computes their logits, softmax and CE gradient
+// alone; the one cross-CU exchange of a step is the partial gradient of p (N values):
+// wave 0 publishes its workgroup's sum (8-byte {tag, value} granules, as the multi-CU
+// solver), reads the K partials back and folds them in workgroup order -- the same bits in
+// every workgroup, so every copy of p and of the momentum buffer stays identical.  Per step a
+// CU gathers 16*C*N*4 / K bytes of Z instead of all of it (one CU gathering random rows is the
+// register solver's bound, section 4.5 of DESIGN.md), for one hop of N values.
+// 8*K blocks are launched and those with blockIdx % 8 == 0 take part (one XCD under
+// round-robin placement; speed only).  Spins are bounded; a timeout sets the error word
+// and poisons p with NaN.
+// Measured (r02ae/af): no faster than the register solver at config 2 (2.40 vs 2.45 us per
+// step at K = 4; 3.0 at K = 8, 4.4 at K = 16) -- the hop costs what the split gather saves
+// (DESIGN.md section 4.5), so it runs only when forced (FS_MIX_SOLVER=rows).
+// ----------------------------------------------------------------------------
+// Row-split solver's exchange: publish this workgroup's partial gradient (NK values per lane,
+// lanes' clients n0 + j) under `tag`, read the K partials -- all granules issued at once, the
+// missing ones re-read -- and fold them in workgroup order into tot.
+template <int NK, int KMAX>
+__device__ __forceinline__ void mrr_exchange(unsigned long long* slot, int k, int K, int n0, unsigned tag,
+                                             const float (&gk)[NK], float (&tot)[NK], bool& dead,
+                                             unsigned spin_limit, unsigned* err) {
+  constexpr int SLOT = NK * 64;
+#pragma unroll
+  for (int j = 0; j < NK; ++j)
+    __hip_atomic_store(slot + (int64_t)k * SLOT + n0 + j,
+                       ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(gk[j]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long gr[KMAX][NK];
+  unsigned spins = 0;
+  for (;;) {
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q)
+#pragma unroll
+      for (int j = 0; j < NK; ++j)
+        if (q < K && q != k)
+          gr[q][j] = __hip_atomic_load(slot + (int64_t)q * SLOT + n0 + j, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q)
+#pragma unroll
+      for (int j = 0; j < NK; ++j)
+        if (q < K && q != k) ok = ok && (unsigned)(gr[q][j] >> 32) == tag;
+    if (ok || dead) break;
+    if (++spins > spin_limit) {
+      dead = true;
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q)
+      if (q < K) a += q == k ? gk[j] : __uint_as_float((unsigned)gr[q][j]);
+    tot[j] = a;
+  }
+}
+
+template <int NK, int CP, int CL, int RW, int DEPTH>
+__global__ __launch_bounds__(RW * 64) void mix_solve_rows_kernel(const float* __restrict__ Z,
+                                                                const int32_t* __restrict__ y,
+                                                                const int32_t* __restrict__ perms, int N, int C,
+                                                                int nv, int epochs, int Bv, float lr, float mom,
+                                                                float* __restrict__ p, float* __restrict__ buf,
+                                                                int* __restrict__ first_flag,
+                                                                unsigned long long* __restrict__ xbuf,
+                                                                unsigned* __restrict__ err, int K,
+                                                                unsigned spin_limit) {
+  static_assert(CL <= CP && CP <= 32 && (CP & (CP - 1)) == 0, "class padding");
+  static_assert(DEPTH * (CL + 2) <= 63, "ring vs the vmcnt window");
+  if (blockIdx.x % 8) return;
+  typedef typename MRVec<NK>::T vec;
+  constexpr int LPC = 64 / CP;
+  constexpr int SLOT = NK * 64;                     // granules per workgroup and parity
+  constexpr int KMAX = 16 / RW;
+  __shared__ __attribute__((aligned(16))) float gpart[RW > 1 ? 2 : 1][RW][NK * 64];
+  __shared__ __attribute__((aligned(16))) float gtot[RW > 1 ? 2 : 1][NK * 64];
+  const int k = blockIdx.x / 8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = k * RW + w;                       // this wave's batch row
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int n0 = NK * lane;
+  float pr[NK], br[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    const int n = n0 + j;
+    pr[j] = n < N ? p[n] : 0.f;
+    br[j] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  const float invB = 1.0f / (float)Bv;
+  const uint32_t nbyte = 4u * (uint32_t)min(n0, ldN - NK);
+  bool dead = false;
+  if (spin_limit == 0 && k == 0 && tid == 0 && total > 0)   // test knob: report an injected timeout
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  vec zr[DEPTH][CL];
+  int lab[DEPTH], idxr[DEPTH];
+  auto row_of = [&](int st) -> int {               // perms entry of lane `lane` (a batch row) in step st
+    const int ep = st / nbat, sb = st - ep * nbat;
+    const int b = sb * Bv + lane;
+    const int64_t at = (lane < Bv && b < nv && st < total) ? (int64_t)ep * nv + b : 0;
+    return perms[at];
+  };
+#define MRR_ISSUE(R_, IDXV_)                                                               \
+  {                                                                                        \
+    const int vrow_ = __builtin_amdgcn_readlane((IDXV_), row < 16 ? row : 0);              \
+    const char* zp_ = reinterpret_cast<const char*>(Z + (int64_t)vrow_ * CN);              \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                       \
+      const char* zc_ = zp_ + 4 * (int64_t)(min(c, C - 1) * ldN);                          \
+      zr[R_][c] = *reinterpret_cast<const vec*>(__builtin_assume_aligned(zc_ + nbyte, 4 * NK)); \
+    }                                                                                      \
+    lab[R_] = y[(IDXV_)];                                                                  \
+  }
+  {
+#pragma unroll
+    for (int r0 = 0; r0 < DEPTH; ++r0) {
+      const int iv = row_of(r0);
+      MRR_ISSUE(r0, iv);
+    }
+#pragma unroll
+    for (int r0 = 0; r0 < DEPTH; ++r0) idxr[r0] = row_of(DEPTH + r0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): the loop inherits only its own order
+  }
+  int s = 0;
+#define MRR_STEP(R_)                                                                       \
+  {                                                                                        \
+    if (s >= total) break;                                                                 \
+    const int idx_cur = idxr[R_];                                                          \
+    idxr[R_] = row_of(s + 2 * DEPTH);                                                      \
+    const int bc = min(Bv, nv - (s % nbat) * Bv);                                          \
+    float gme[NK];                                                                         \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                           \
+    if (row < bc) {                                                                        \
+      float v[CP];                                                                         \
+      _Pragma("unroll") for (int c = 0; c < CP; ++c) {                                     \
+        float a = 0.f;                                                                     \
+        if (c < CL) {                                                                      \
+          _Pragma("unroll") for (int j = 0; j < NK; ++j) a += mr_el<NK>(zr[R_][c], j) * pr[j]; \
+        }                                                                                  \
+        v[c] = a;                                                                          \
+      }                                                                                    \
+      const float o = class_totals<CP>(v, lane);                                           \
+      const int cls = lane / LPC;                                                          \
+      const bool real = cls < C;                                                           \
+      const float m = class_max<LPC>(real ? o : -INFINITY, lane);                          \
+      const float e = class_sum<LPC>(real ? expf(o - m) : 0.f, lane);                      \
+      const float lse = logf(e);                                                           \
+      const float invb = bc == Bv ? invB : 1.0f / (float)bc;                               \
+      const int yy = __builtin_amdgcn_readlane(lab[R_], row);                              \
+      const float g = (cls == yy ? -invb : 0.f) + expf(o - m - lse) * invb;                \
+      _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                     \
+        if (c < C) {                                                                       \
+          const float gc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(            \
+              __builtin_bit_cast(int, g), c * LPC));                                       \
+          _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] += gc * mr_el<NK>(zr[R_][c], j); \
+        }                                                                                  \
+      }                                                                                    \
+    }                                                                                      \
+    const int par = s & 1;                                                                 \
+    float tot[NK];                                                                         \
+    if constexpr (RW > 1) {                                                                \
+      _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[par][w][n0 + j] = gme[j];       \
+      lds_barrier();                                                                       \
+    }                                                                                      \
+    if (RW == 1 || w == 0) {                                                               \
+      float gk[NK];                                                                        \
+      _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                     \
+        float a = gme[j];                                                                  \
+        if constexpr (RW > 1) {                                                            \
+          a = 0.f;                                                                         \
+          _Pragma("unroll") for (int i = 0; i < RW; ++i) a += gpart[par][i][n0 + j];       \
+        }                                                                                  \
+        gk[j] = a;                                                                         \
+      }                                                                                    \
+      mrr_exchange<NK, KMAX>(xbuf + (int64_t)par * K * SLOT, k, K, n0, (unsigned)s + 1u, gk, tot, \
+                             dead, spin_limit, err);                                       \
+      if constexpr (RW > 1) {                                                              \
+        _Pragma("unroll") for (int j = 0; j < NK; ++j) gtot[par][n0 + j] = tot[j];         \
+      }                                                                                    \
+    }                                                                                      \
+    if constexpr (RW > 1) {                                                                \
+      lds_barrier();                                                                       \
+      _Pragma("unroll") for (int j = 0; j < NK; ++j) tot[j] = gtot[par][n0 + j];           \
+    }                                                                                      \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j)                                         \
+      if (n0 + j < N) momentum_step(pr[j], br[j], tot[j], first, mom, lr);                 \
+    first = 0;                                                                             \
+    /* the ring slot refills only now: the exchange's polls would wait behind it (refilling \
+       before the exchange measured the same, r02af) */                                    \
+    MRR_ISSUE(R_, idx_cur);                                                                \
+    ++s;                                                                                   \
+  }
+  for (;;) {
+    MRR_STEP(0)
+    if constexpr (DEPTH > 1) MRR_STEP(1)
+    if constexpr (DEPTH > 2) MRR_STEP(2)
+  }
+#undef MRR_STEP
+#undef MRR_ISSUE
+  if (k == 0 && w == 0) {
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int n = n0 + j;
+      if (n < N) {
+        p[n] = dead ? __int_as_float(0x7fc00000) : pr[j];
+        buf[n] = br[j];
+      }
+    }
+    if (lane == 0 && total > 0) *first_flag = 0;
+  }
+}
+
+// exchange granules of the row-split solver: [2][K][64*NK], zeroed before every launch
+static int64_t mrr_xbytes(int N) {
+  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : 4);
+  return (int64_t)sizeof(unsigned long long) * 2 * 16 * 64 * nk;
+}
+
+static bool mrr_covers(int N, int C, int Bv) { return Bv <= 16 && N <= 256 && C <= 16; }
+
+// rows per workgroup: FS_MIX_ROWS_RW=1|2|4|8 (diagnostics), default 4 -- r02ae/af, N = 100,
+// C = 10, us per step, RW = 1 / 2 / 4 / 8 (K = 16 / 8 / 4 / 2): 4.41 / 3.00 / 2.40 / 2.46
+// (the register solver: 2.45)
+static int mrr_rw() {
+  const char* env = getenv("FS_MIX_ROWS_RW");
+  const int r = env ? atoi(env) : 4;
+  return (r == 1 || r == 2 || r == 8) ? r : 4;
+}
+
+template <int NK, int CP, int CL, int RW>
+static void launch_mix_rows(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                            int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                            unsigned long long* xbuf, unsigned* err, unsigned spin_limit) {
+  constexpr int depth = 3 * (CL + 2) <= 63 ? 3 : 2;
+  const int K = (Bv + RW - 1) / RW;
+  hipLaunchKernelGGL((mix_solve_rows_kernel<NK, CP, CL, RW, depth>), dim3(8 * K), dim3(RW * 64), 0, st, Z, y,
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, xbuf, err, K, spin_limit);
+}
+
+static unsigned mc_spin_limit();
+
+// row-split solver for (N, C, Bv) if an instance covers it: 1 launched, 0 not covered, < 0 error
+static int mix_solve_rows(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                          int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                          void* d_ws, int64_t ws_bytes, int64_t err_bytes) {
+  if (!mrr_covers(N, C, Bv)) return 0;
+  const int64_t xbytes = mrr_xbytes(N);
+  if (!d_ws || ws_bytes < xbytes + err_bytes)
+    return fail(FS_EINVAL, "fs_mix_solve: workspace too small (see fs_mix_solve_ws_bytes)");
+  unsigned long long* ws = reinterpret_cast<unsigned long long*>(d_ws);
+  unsigned* err = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - err_bytes);
+  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : 4);
+  const int rw = mrr_rw();
+  const unsigned spin_limit = mc_spin_limit();
+  bool launched = false;
+#define MRR_CASE(NK_, CP_, CL_)                                                                            \
+  if (!launched && nk == NK_ && C <= CL_) {                                                                \
+    hipError_t e = hipMemsetAsync(ws, 0, (size_t)xbytes, st);                                              \
+    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));      \
+    if (rw == 1)                                                                                           \
+      launch_mix_rows<NK_, CP_, CL_, 1>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
+                                        spin_limit);                                                       \
+    else if (rw == 2)                                                                                      \
+      launch_mix_rows<NK_, CP_, CL_, 2>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
+                                        spin_limit);                                                       \
+    else if (rw == 8)                                                                                      \
+      launch_mix_rows<NK_, CP_, CL_, 8>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
+                                        spin_limit);                                                       \
+    else                                                                                                   \
+      launch_mix_rows<NK_, CP_, CL_, 4>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
+                                        spin_limit);                                                       \
+    launched = true;                                                                                       \
+  }
+  MRR_CASE(1, 2, 2) MRR_CASE(1, 4, 4) MRR_CASE(1, 8, 8) MRR_CASE(1, 16, 10) MRR_CASE(1, 16, 16)
+  MRR_CASE(2, 2, 2) MRR_CASE(2, 4, 4) MRR_CASE(2, 8, 8) MRR_CASE(2, 16, 10) MRR_CASE(2, 16, 16)
+  MRR_CASE(4, 2, 2) MRR_CASE(4, 4, 4) MRR_CASE(4, 8, 8) MRR_CASE(4, 16, 10)
+#undef MRR_CASE
+  return launched ? 1 : 0;
+}
+
+// ----------------------------------------------------------------------------
 // p-solve, register-resident form 2 (Bv <= 16, C <= CL <= 10, N <= 64*NK): the register
 // solver above is VALU-bound (rocprofv3: the SIMDs' vector pipes ~80 % busy at config 2);
 // this form does the same arithmetic in fewer vector instructions per step:
@@ -1247,7 +1536,9 @@ extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   if (N < 1) return MC_ERR_BYTES;
   const int S = mc_slice(N);
   const int K = S ? (mix_ldn(N) + S - 1) / S : 0;
-  return (mc_covers(N, C, Bv) ? mc_xbytes(K) : 0) + MC_ERR_BYTES;
+  const int64_t mc = mc_covers(N, C, Bv) ? mc_xbytes(K) : 0;
+  const int64_t rows = mrr_covers(N, C, Bv) ? mrr_xbytes(N) : 0;
+  return std::max(mc, rows) + MC_ERR_BYTES;
 }
 
 extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val, float* d_Z,
@@ -1297,6 +1588,16 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     t_last_solver = 1;
     FS_LAUNCH_CHECK();
     return FS_OK;
+  }
+  if (want == "rows") {
+    const int rc = mix_solve_rows(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
+                                  d_first, d_ws, ws_bytes, MC_ERR_BYTES);
+    if (rc < 0) return rc;
+    if (rc == 1) {
+      t_last_solver = 7;
+      FS_LAUNCH_CHECK();
+      return FS_OK;
+    }
   }
   if (want == "auto" || want == "mc") {
     const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,

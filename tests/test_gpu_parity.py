@@ -390,6 +390,34 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S, hops):
     assert mode == 2, mode             # the multi-CU solver ran (a timed-out spin raises in check_errors)
 
 
+@pytest.mark.parametrize('rw', [1, 2, 4, 8])
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (100, 10, 517, 16),     # config 2 shape: NK = 2, CP = 16
+    (10, 2, 203, 16),       # config 1 shape: NK = 1, CP = 2
+    (200, 4, 301, 16),      # NK = 4
+    (129, 3, 77, 8),        # Bv < 16: fewer workgroups, ragged last batch
+    (5, 3, 40, 7),          # Bv = 7: the last workgroup's rows partly idle
+    (37, 16, 90, 16),       # C = 16: every class slot real
+])
+def test_mix_solve_rows(amd, monkeypatch, N, C, nv, Bv, rw):
+    """fs_mix_solve's row-split solver (batch rows over K = Bv / rw workgroups, one exchange of
+    the N partial gradients per step) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'rows')
+    monkeypatch.setenv('FS_MIX_ROWS_RW', str(rw))
+    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.1 if N == 200 else 0.5)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'rows'
+
+
+def test_mix_solve_rows_timeout_raises(amd, monkeypatch):
+    """A timed-out exchange of the row-split solver sets the error word: check_errors raises."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'rows')
+    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
+    with pytest.raises(amd.lib.FedsimError):
+        test_mix_solve_variants(amd, 100, 10, 64, 16)
+    monkeypatch.delenv('FS_SPIN_LIMIT')
+    test_mix_solve_variants(amd, 100, 10, 64, 16)
+
+
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
                                         ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('reg2-select', 100, 10),
                                         ('reg2-select', 129, 3)])
