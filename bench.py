@@ -190,8 +190,7 @@ def fedamw_leg(d, args, dev, rounds, warmup=1):
             'p_solve_ms': solve_ms, 'p_solve_steps': steps, 'p_solve_us_per_step': 1e3 * solve_ms / steps,
             'p_solve_steps_per_s': steps / (solve_ms * 1e-3), 'p_solve_gbs': solve_bytes / (solve_ms * 1e-3) / 1e9,
             'p_solve_frac_hbm': solve_bytes / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            'p_solver': {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global'}.get(
-                fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
+            'p_solver': fedamw_amd._lib.SOLVER_NAMES.get(fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
             'n_val': nv, 'inner_epochs': R, 'rounds_timed': rounds}
 
 

@@ -158,14 +158,17 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * buf = first ? grad : momentum*buf + grad; p -= lr_p*buf.  d_p, d_buf [N] are
  * updated in place; *d_first (int) is read and cleared (the momentum buffer of
  * torch.optim.SGD starts empty, tools.py:423).  A single persistent workgroup
- * where a register-resident instance covers (N, C, Bv); otherwise (Bv <= 16,
+ * where a register-resident instance covers (N, C, Bv) -- for N <= 128 the quarter-wave
+ * solver (4 batch rows per wave), with 4 L2 prefetch helper workgroups on its XCD that
+ * only load (FS_MIX_PF_H=<n> sets their number, 0 = none; their progress word is byte
+ * 128 of the error block); otherwise (Bv <= 16,
  * C <= 16, N <= 2048) K <= 32 workgroups that split the clients and exchange
  * partial logits every step (slices of S >= 16 clients: reduce-scatter to owner workgroups, then an
  * all-gather of the totals; FS_MIX_MC_HOPS=1 forces the one-hop all-to-all);
  * otherwise one LDS-staged / global workgroup.
  * d_ws: fs_mix_solve_ws_bytes(N, C, Bv) bytes, zeroed once at allocation (the multi-CU
  * exchange granules + the error block; a timed-out exchange also writes NaN into d_p).
- * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=wave|reg2|reg|mc|staged|global
+ * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=wave|quad|reg2|reg|mc|staged|global
  * forces one solver (FS_MIX_SWAP=0: reg2 without the permlane swap-add levels).
  * ------------------------------------------------------------------------- */
 int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv);
@@ -176,7 +179,8 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
 /* Diagnostic (host state only): the solver the calling thread's last fs_mix_solve
  * launched -- 1 register-resident (one row per wave), 2 multi-CU, 3 LDS-staged, 4 global,
  * 5 register-resident form 2 (two rows per wave, Bv <= 16, C <= 10), 6 one wave (N <= 16,
- * C <= 4, Bv <= 16); 0 = none yet. */
+ * C <= 4, Bv <= 16), 7 row-split (forced only), 8 quarter-wave (N <= 64 with C <= 16, or
+ * N <= 128 with C <= 10; Bv <= 16); 0 = none yet. */
 int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *

@@ -56,7 +56,7 @@ ABI_VERSION = 6
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
-SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows'}
+SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows', 8: 'quad'}
 
 
 class PlanDesc(C.Structure):

@@ -84,4 +84,68 @@ __device__ __forceinline__ float class_sum(float x, int lane) {
   return x;
 }
 
+// reduce-scatter level at lane distance OFF over pairs (a, b): lanes with (lane & OFF) keep b
+template <int OFF, bool SWAP>
+__device__ __forceinline__ float rs_level(float a, float b, int lane) {
+  if constexpr (SWAP && (OFF == 32 || OFF == 16)) {
+    // inline asm, not the builtin: with a constant-zero partner (padding classes) hipcc
+    // 7.2 drops the builtin's second result and sums r0 + 0.  The pad inside the string is
+    // the 2 wait states a VALU write of either operand needs before v_permlane*_swap reads it.
+    if constexpr (OFF == 32)
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    else
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return a + b;
+  } else {
+    return rs_pair(a, b, OFF, lane);
+  }
+}
+
+// one reduce-scatter level of a 16-lane row at lane distance 8 or 4: two DPP adds, each
+// writing the lanes (DPP banks) that keep one element of the pair: dst = partner's copy of
+// that element + own copy (lanes with the OFF bit clear keep lo, the others hi)
+template <int OFF>
+__device__ __forceinline__ float rs_bank(float lo, float hi) {
+  float r;
+  if constexpr (OFF == 8)
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %0, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xc"
+        : "=&v"(r)
+        : "v"(lo), "v"(hi));
+  else
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %1, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %0, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa"
+        : "=&v"(r)
+        : "v"(lo), "v"(hi));
+  return r;
+}
+
+// max / sum over the 16 lanes of a DPP row (rotations 8 and 4, then the quad butterflies:
+// every lane of the row ends with bitwise the same value)
+template <bool MAX>
+__device__ __forceinline__ float row16_all(float x) {
+  x = MAX ? fmaxf(x, dpp<0x128>(x)) : x + dpp<0x128>(x);   // row_ror:8
+  x = MAX ? fmaxf(x, dpp<0x124>(x)) : x + dpp<0x124>(x);   // row_ror:4
+  x = MAX ? fmaxf(x, dpp<0x4E>(x)) : x + dpp<0x4E>(x);     // quad xor 2
+  x = MAX ? fmaxf(x, dpp<0xB1>(x)) : x + dpp<0xB1>(x);     // quad xor 1
+  return x;
+}
+
+// the two values of a permlane swap of x with itself: lo = x of the lane group with the
+// OFF bit clear, hi = x of the group with it set (OFF = 16: rows; 32: halves)
+template <int OFF>
+__device__ __forceinline__ void gather_pair(float x, float& lo, float& hi) {
+  float a = x, b = x;
+  if constexpr (OFF == 32)
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  lo = a;
+  hi = b;
+}
+
 }  // namespace fs

@@ -326,9 +326,13 @@ __global__ __launch_bounds__(MS_THREADS) void mix_solve_staged_kernel(const floa
 //   softmax   max / sum over the class groups (xor exchanges); the CE gradient of lane l's
 //             class, g = (softmax - onehot) / bc (torch's log_softmax backward)
 //   grad_p    g[c] broadcast by readlane; lane partial sum_c g[c] Z[v_b][c][n_j]; wave
-//             partials through LDS (double-buffered by step parity: ONE raw barrier per
-//             step), summed in wave order by every wave, then the momentum step
-//             (torch.optim.SGD, two roundings).
+//             partials through LDS; after a raw barrier each client's 16 partials are
+//             folded ONCE (16/NK threads: NK partials each in wave order, then a fixed lane
+//             tree), its owner thread takes the momentum step (torch.optim.SGD, two
+//             roundings) and publishes p[n] in LDS; after a second barrier every wave reads
+//             its lanes' p back.  (Round 2's form -- every wave folding all 16 x 64NK
+//             partials itself, one barrier -- spent ~2,000 of a step's ~5,900 cycles in LDS
+//             reads: 128 KB per step at N = 100; r02s2c stamps.)
 // Z rows never touch LDS: each step's row segment is ONE dword / dwordx2 / dwordx4 load per
 // class per lane into a 3-deep register ring (the loads of step s+3 are issued as soon as
 // step s's data is consumed; CL + 2 loads per step keep 3 steps under the 63-deep vmcnt
@@ -361,6 +365,65 @@ constexpr int MR_WAVES = 16;
 #define MR_STAMP(k)
 #endif
 
+// ----------------------------------------------------------------------------
+// L2 prefetch helpers of the single-CU solvers.  One CU gathers random Z rows from the
+// Infinity Cache at ~33.5 GB/s but from its XCD's L2 at 66-73 GB/s (MI355X_MICROARCH.md,
+// "Indexed rows"); the register solver is bound by the former.  The
+// step order is known before the launch (the perms), so H helper workgroups on the solver's
+// XCD (blockIdx % 8 == 0 under round-robin placement) load the Z rows of the steps ahead
+// of the solver into that L2: helper h takes steps h, h + H, ..., each wave one batch row,
+// and stays at most `lead` steps ahead of the solver's progress word (wave 0 of the solver
+// stores its step count every 4 steps).  Helpers change no bytes the solver reads or
+// writes -- they only warm the cache -- so results are identical with any H (speed only).
+// Every wait is bounded and a helper that starts late (after the solver) or falls behind
+// skips to the solver's position; it exits once the solver's count reaches the total.
+// ----------------------------------------------------------------------------
+constexpr int PF_SPIN_LIMIT = 1 << 22;
+
+__device__ __noinline__ void mix_prefetch_helper(const float* __restrict__ Z, const int32_t* __restrict__ perms,
+                                                 int N, int C, int nv, int epochs, int Bv, int h, int H, int lead,
+                                                 const unsigned* prog) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nw = blockDim.x >> 6;
+  const int CN4 = C * mix_ldn(N) / 4;             // float4 per Z row (ldN % 4 == 0)
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  unsigned seen = 0;
+  for (int t = h; t < total; t += H) {
+    int spins = 0;
+    while ((unsigned)t >= seen + (unsigned)lead) {   // pace: at most `lead` steps ahead
+      seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if ((unsigned)t < seen + (unsigned)lead) break;
+      if (++spins > PF_SPIN_LIMIT) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (seen >= (unsigned)total) return;           // the solver is done
+    if ((unsigned)t < seen) {                      // fell behind: skip to the solver's step
+      t += (int)((seen - (unsigned)t + H - 1) / H) * H;
+      if (t >= total) return;
+    }
+    const int ep = t / nbat, sb = t - ep * nbat;
+    const int bc = min(Bv, nv - sb * Bv);
+    for (int r = w; r < bc; r += nw) {
+      const int row = perms[(int64_t)ep * nv + sb * Bv + r];
+      const float4* zr = reinterpret_cast<const float4*>(Z + (int64_t)row * (4 * CN4));
+      for (int i0 = 0; i0 < CN4; i0 += 256) {    // 4 loads in flight per lane
+        float4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = zr[min(i0 + 64 * k + lane, CN4 - 1)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(v[k].x));   // keep the loads
+      }
+    }
+  }
+}
+
+// the solver's side: publish the number of completed steps (vector store, relaxed agent scope)
+__device__ __forceinline__ void mix_publish_progress(unsigned* prog, int s) {
+  if (threadIdx.x == 0) __hip_atomic_store(prog, (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NK> struct MRVec;
 template <> struct MRVec<1> { typedef float T; };
 template <> struct MRVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
@@ -378,12 +441,20 @@ __global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const floa
                                                                      int C, int nv, int epochs, int Bv, float lr,
                                                                      float mom, float* __restrict__ p,
                                                                      float* __restrict__ buf,
-                                                                     int* __restrict__ first_flag) {
+                                                                     int* __restrict__ first_flag,
+                                                                     unsigned* __restrict__ pf_prog, int pf_h,
+                                                                     int pf_lead) {
   static_assert(CL <= CP && CP <= 32 && (CP & (CP - 1)) == 0, "class padding");
   static_assert(MR_DEPTH * (CL + 2) <= 63 && (MR_DEPTH == 2 || MR_DEPTH == 3), "ring vs the vmcnt window");
+  if (blockIdx.x != 0) {                           // L2 prefetch helpers (speed only)
+    if (pf_prog && blockIdx.x % 8 == 0)
+      mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, blockIdx.x / 8 - 1, pf_h, pf_lead, pf_prog);
+    return;
+  }
   typedef typename MRVec<NK>::T vec;
   constexpr int LPC = 64 / CP;                     // lanes per class after the reduce-scatter
-  __shared__ __attribute__((aligned(16))) float gpart[2][MR_WAVES][NK * 64];
+  __shared__ __attribute__((aligned(16))) float gpart[MR_WAVES][NK * 64];
+  __shared__ __attribute__((aligned(16))) float pnew[NK * 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ldN = mix_ldn(N);
@@ -391,13 +462,15 @@ __global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const floa
   const int nbat = (nv + Bv - 1) / Bv;
   const int total = epochs * nbat;
   const int n0 = NK * lane;                        // this lane's first client
-  float pr[NK], br[NK];
+  float pr[NK];
 #pragma unroll
-  for (int j = 0; j < NK; ++j) {
-    const int n = n0 + j;
-    pr[j] = n < N ? p[n] : 0.f;                    // p stays 0 on padding clients
-    br[j] = n < N ? buf[n] : 0.f;
-  }
+  for (int j = 0; j < NK; ++j) pr[j] = n0 + j < N ? p[n0 + j] : 0.f;   // p stays 0 on padding clients
+  // the update's owner of client `cn`: TPC = 16 / NK consecutive threads fold its 16 wave
+  // partials (NK each, then a lane tree); the first of them keeps its p and momentum entry
+  constexpr int TPC = MR_WAVES / NK;
+  const int cn = tid / TPC, cq = tid % TPC;
+  float po = (cq == 0 && cn < N) ? p[cn] : 0.f;
+  float bo = (cq == 0 && cn < N) ? buf[cn] : 0.f;
   int first = *first_flag;
   const float invB = 1.0f / (float)Bv;            // 1/|batch| of every full batch
   // lane byte offset inside a class segment; lanes past ldN re-read the last vector (p = 0)
@@ -478,20 +551,30 @@ __global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const floa
       }                                                                                    \
     }                                                                                      \
     MR_STAMP(2)                                                                            \
-    const int par = s & 1;                                                                 \
-    _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[par][w][n0 + j] = gme[j];         \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[w][n0 + j] = gme[j];              \
     MR_ISSUE(R_, idx_cur);                                                                 \
     MR_STAMP(3)                                                                            \
     lds_barrier();                 /* not __syncthreads: that would drain the ring */     \
     MR_STAMP(4)                                                                            \
-    _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                       \
-      float gp = 0.f;                                                                      \
-      _Pragma("unroll") for (int i = 0; i < MR_WAVES; ++i) gp += gpart[par][i][n0 + j];    \
-      if (n0 + j < N) momentum_step(pr[j], br[j], gp, first, mom, lr);                     \
+    {                              /* fold once per client, update at its owner */       \
+      float gp = gpart[cq * NK][cn];                                                       \
+      _Pragma("unroll") for (int i = 1; i < NK; ++i) gp += gpart[cq * NK + i][cn];         \
+      _Pragma("unroll") for (int off = 1; off < TPC; off <<= 1) gp += xor_get(gp, off, lane); \
+      if (cq == 0) {                                                                       \
+        if (cn < N) momentum_step(po, bo, gp, first, mom, lr);                             \
+        pnew[cn] = po;                                                                     \
+      }                                                                                    \
+    }                                                                                      \
+    lds_barrier();                                                                         \
+    if constexpr (NK == 1) pr[0] = pnew[n0];                                               \
+    else {                                                                                 \
+      const vec pv = *reinterpret_cast<const vec*>(&pnew[n0]);                             \
+      _Pragma("unroll") for (int j = 0; j < NK; ++j) pr[j] = mr_el<NK>(pv, j);             \
     }                                                                                      \
     first = 0;                                                                             \
     MR_STAMP(5)                                                                            \
     ++s;                                                                                   \
+    if (pf_prog && (s & 3) == 0) mix_publish_progress(pf_prog, s);                         \
   }
 #ifdef FS_MIX_STAMPS
   unsigned long long mr_acc[5] = {0, 0, 0, 0, 0}, mr_prev = 0;
@@ -504,15 +587,12 @@ __global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const floa
   }
 #undef MR_STEP
 #undef MR_ISSUE
+  if (pf_prog) mix_publish_progress(pf_prog, total);   // releases the helpers
+  if (cq == 0 && cn < N) {
+    p[cn] = po;
+    buf[cn] = bo;
+  }
   if (w == 0) {
-#pragma unroll
-    for (int j = 0; j < NK; ++j) {
-      const int n = n0 + j;
-      if (n < N) {
-        p[n] = pr[j];
-        buf[n] = br[j];
-      }
-    }
     if (lane == 0 && total > 0) *first_flag = 0;
 #ifdef FS_MIX_STAMPS
     if (lane < 5) reinterpret_cast<unsigned long long*>(buf + N + 8)[lane] = mr_acc[lane];
@@ -520,23 +600,31 @@ __global__ __launch_bounds__(MR_WAVES * 64) void mix_solve_reg_kernel(const floa
   }
 }
 
+struct MixPrefetch {
+  unsigned* prog;   // progress word (null: no helpers)
+  int h, lead;      // helper workgroups, steps ahead
+};
+
 template <int NK, int CP, int CL>
 static void launch_mix_reg(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
-                           int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+                           int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                           const MixPrefetch& pf) {
   constexpr int depth = 3 * (CL + 2) <= 63 ? 3 : 2;   // CL + 2 loads per step stay in the vmcnt window
-  hipLaunchKernelGGL((mix_solve_reg_kernel<NK, CP, CL, depth>), dim3(1), dim3(MR_WAVES * 64), 0, st, Z, y, perms,
-                     N, C, nv, epochs, Bv, lr, mom, p, buf, first);
+  const int blocks = pf.prog ? 8 * pf.h + 1 : 1;
+  hipLaunchKernelGGL((mix_solve_reg_kernel<NK, CP, CL, depth>), dim3(blocks), dim3(MR_WAVES * 64), 0, st, Z, y,
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, pf.prog, pf.h, pf.lead);
 }
 
 // register-resident solver for (N, C, Bv) if an instance covers it
 static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
-                          int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first) {
+                          int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                          const MixPrefetch& pf) {
   if (Bv > MR_WAVES) return false;
   const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : (N <= 256 ? 4 : 0));
-#define MR_CASE(NK_, CP_, CL_)                                                                  \
-  if (nk == NK_ && C <= CL_) {                                                                  \
-    launch_mix_reg<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first); \
-    return true;                                                                                \
+#define MR_CASE(NK_, CP_, CL_)                                                                      \
+  if (nk == NK_ && C <= CL_) {                                                                      \
+    launch_mix_reg<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, pf); \
+    return true;                                                                                    \
   }
   // (the ring holds DEPTH * CL * NK floats per lane: larger shapes take the LDS-staged solver)
   MR_CASE(1, 2, 2) MR_CASE(1, 4, 4) MR_CASE(1, 8, 8) MR_CASE(1, 16, 10) MR_CASE(1, 16, 16) MR_CASE(1, 32, 24)
@@ -852,23 +940,6 @@ static int mix_solve_rows(hipStream_t st, const float* Z, const int32_t* y, cons
 // ----------------------------------------------------------------------------
 constexpr int M2_WAVES = 8;
 
-// reduce-scatter level at lane distance OFF over pairs (a, b): lanes with (lane & OFF) keep b
-template <int OFF, bool SWAP>
-__device__ __forceinline__ float rs_level(float a, float b, int lane) {
-  if constexpr (SWAP && (OFF == 32 || OFF == 16)) {
-    // inline asm, not the builtin: with a constant-zero partner (padding classes) hipcc
-    // 7.2 drops the builtin's second result and sums r0 + 0.  The pad inside the string is
-    // the 2 wait states a VALU write of either operand needs before v_permlane*_swap reads it.
-    if constexpr (OFF == 32)
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    else
-      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    return a + b;
-  } else {
-    return rs_pair(a, b, OFF, lane);
-  }
-}
-
 // class_totals of lanes.h for two independent rows at once (the levels interleave)
 template <int CP, bool SWAP>
 __device__ __forceinline__ void class_totals2(float (&v0)[CP], float (&v1)[CP], int lane, float& o0, float& o1) {
@@ -1086,6 +1157,275 @@ static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, con
   M2_CASE(2, 2, 2) M2_CASE(2, 4, 4) M2_CASE(2, 8, 8) M2_CASE(2, 16, 10)
   M2_CASE(4, 2, 2) M2_CASE(4, 4, 4)
 #undef M2_CASE
+  return false;
+}
+
+// ----------------------------------------------------------------------------
+// p-solve, quarter-wave form "quad" (Bv <= 16, N <= 16*NK, C <= CL <= 16).  The register
+// solvers above are bound by the vector ALU, not by the Z gather: at config 2 a step costs the
+// same 2.36-2.46 us with Z = 51 MB (Infinity Cache) as with Z = 0.5 MB (L2), and with
+// s_memtime stamps the first wave of each SIMD finishes its row ~2,500 cycles before the last
+// (4 waves x ~270 VALU instructions per step on every SIMD; r02s2c/d).  Most of those
+// instructions are the cross-lane reductions of ONE row over 64 lanes.  Here a row takes 16
+// lanes (one DPP row), so one wave instruction advances 4 batch rows at once:
+//   * 4 waves x 4 rows (batch row b = 4w + q for lane group q = lane / 16); lane (q, r) holds
+//     clients n = NK*r + j of its row, every class: the logits' partials are NK-term dot
+//     products, reduce-scattered over the 16 lanes (levels 8 and 4 as two bank-masked DPP
+//     adds each, 2 and 1 in the select form) so that lane r ends with class r's logit;
+//   * softmax max / sum as 4-level DPP all-reduces inside the row (bitwise-identical in
+//     every lane of the row), the CE gradient g of lane r's class;
+//   * the row's g values broadcast through 64 bytes of the wave's own LDS (16 lanes read one
+//     address: no conflict, no barrier), the gradient partials of the NK clients in-lane;
+//   * the 4 rows of a wave folded by a reduce-scatter over the row groups (permlane32 /
+//     permlane16 swaps: lane keeps NK/4 clients), the 4 waves' partials through LDS (ONE
+//     raw barrier per step, double-buffered by step parity), summed in wave order by every
+//     wave -- the same bits everywhere -- then the momentum step on the kept clients and an
+//     all-gather (the same swaps) returns p to the NK-per-lane layout;
+//   * Z through one buffer descriptor (row offset per lane group, class offset scalar), a
+//     DEPTH-deep register ring; row indices and labels per lane, DEPTH steps ahead.
+// Optional L2 prefetch helpers as for the register solver (FS_MIX_PF_H).
+// ----------------------------------------------------------------------------
+constexpr int MQ_WAVES = 4;
+
+template <int NK, int CL, int DEPTH, int SPL>
+__global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
+    const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
+    int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
+    int* __restrict__ first_flag, int z_bytes, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead, int oob) {
+  static_assert(NK == 4 || NK == 8, "clients per lane");
+  static_assert(CL >= 1 && CL <= 16, "classes");
+  static_assert(DEPTH * (CL * NK / 4 + 2) <= 63, "ring vs the vmcnt window");
+  static_assert(SPL >= 1 && SPL <= CL, "issue split");
+  if (blockIdx.x != 0) {                           // L2 prefetch helpers (speed only)
+    if (pf_prog && blockIdx.x % 8 == 0)
+      mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, blockIdx.x / 8 - 1, pf_h, pf_lead, pf_prog);
+    return;
+  }
+  constexpr int NV4 = NK / 4;                      // float4 chunks per class and lane
+  constexpr int KP = NK / 4;                       // clients a lane keeps after the row fold
+  __shared__ __attribute__((aligned(16))) float gx[2][MQ_WAVES][64 * KP];
+  __shared__ __attribute__((aligned(16))) float gb[MQ_WAVES][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r = lane & 15;
+  const int brow = MQ_WAVES * w + q;               // this lane group's batch row
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int bc_tail = nv - (nbat - 1) * Bv;
+  const float invB = 1.0f / (float)Bv;
+  const float invT = 1.0f / (float)bc_tail;
+  const int n0 = NK * r;
+  float pr[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) pr[j] = n0 + j < N ? p[n0 + j] : 0.f;   // p = 0 on padding clients
+  // kept clients after the fold over the row groups: j = (q >> 1) NK/2 + (q & 1) NK/4 + i
+  const int kj0 = (q >> 1) * (NK / 2) + (q & 1) * (NK / 4);
+  float po[KP], bo[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int n = n0 + kj0 + i;
+    po[i] = n < N ? p[n] : 0.f;
+    bo[i] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  // lane byte offsets of its client chunks inside a class segment; a chunk wholly past ldN
+  // gets an offset beyond the buffer's range: the load returns zeros without a memory access
+  // (FS_MIX_QUAD_OOB=0: such chunks re-read the last real one instead -- their p is 0 either way)
+  uint32_t lofs[NV4];
+#pragma unroll
+  for (int h = 0; h < NV4; ++h)
+    lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : (oob ? 0x80000000u : 4u * (uint32_t)(ldN - 4));
+  int sofs[CL];
+#pragma unroll
+  for (int c = 0; c < CL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * ldN);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
+  // fetch cursor: the step whose row indices are read next (stays on the last step at the end)
+  int fst = 0, fep = 0, fsb = 0;
+  auto fetch_row = [&]() -> int {
+    const int base = fep * nv + fsb * Bv;
+    const int bc = min(Bv, nv - fsb * Bv);
+    const int row = perms[base + (brow < bc ? brow : 0)];   // rows past the batch: its first (masked)
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+    return row;
+  };
+  floatx4 zr[DEPTH][CL][NV4];
+  int idxq[DEPTH], labq[DEPTH];
+#define MQ_ISSUE(R_, ROW_, C0_, C1_)                                                         \
+  {                                                                                          \
+    const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
+    _Pragma("unroll") for (int c = C0_; c < C1_; ++c) {                                      \
+      _Pragma("unroll") for (int h = 0; h < NV4; ++h) zr[R_][c][h] = __builtin_bit_cast(     \
+          floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[h], sofs[c], 0));   \
+    }                                                                                        \
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) {
+    const int row = fetch_row();
+    labq[k] = y[row];
+    MQ_ISSUE(k, row, 0, CL);
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) idxq[k] = fetch_row();
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): the loop inherits only its own order
+  int csb = 0;
+  int s = 0;
+  int late_row = 0;                                 // row of the step whose late classes are pending
+#ifdef FS_MIX_STAMPS
+  unsigned long long mr_acc[6] = {0, 0, 0, 0, 0, 0}, mr_prev = 0;
+#endif
+#define MQ_STEP(R_)                                                                          \
+  {                                                                                          \
+    if (s >= total) break;                                                                   \
+    MR_STAMP(0)                                                                              \
+    const int bc = min(Bv, nv - csb * Bv);                                                   \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
+    float v[16];                                                                             \
+    _Pragma("unroll") for (int c = 0; c < 16; ++c) {                                         \
+      float a = 0.f;                                                                         \
+      if (c < CL) {                                                                          \
+        _Pragma("unroll") for (int j = 0; j < NK; ++j) a += zr[R_][c][j >> 2][j & 3] * pr[j]; \
+      }                                                                                      \
+      v[c] = a;                                                                              \
+    }                                                                                        \
+    MR_STAMP(1)                                                                              \
+    /* the late classes of step s - 1 + DEPTH (its early ones went out with the last step) */ \
+    if constexpr (SPL < CL) {                                                                \
+      if (s > 0) MQ_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
+    }                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) v[i] = rs_bank<8>(v[i], v[i + 8]);         \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) v[i] = rs_bank<4>(v[i], v[i + 4]);         \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
+    const float o = rs_pair(v[0], v[1], 1, lane);  /* class r's logit */                     \
+    const bool real = r < C;                                                                 \
+    const float m = row16_all<true>(real ? o : -INFINITY);                                   \
+    const float ssum = row16_all<false>(real ? expf(o - m) : 0.f);                           \
+    const float invb = bc == Bv ? invB : invT;                                               \
+    const float g = (real && brow < bc)                                                      \
+                        ? (r == labq[R_] ? -invb : 0.f) + expf(o - m - logf(ssum)) * invb    \
+                        : 0.f;                                                               \
+    gb[w][lane] = g;                                                                         \
+    float gv[CL];                                                                            \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
+    float gme[NK];                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                             \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
+      _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] += gv[c] * zr[R_][c][j >> 2][j & 3]; \
+    }                                                                                        \
+    MR_STAMP(2)                                                                              \
+    /* slot consumed: refill with step s + DEPTH, then fetch the rows of s + 2 DEPTH */      \
+    labq[R_] = y[idxq[R_]];                                                                  \
+    MQ_ISSUE(R_, idxq[R_], 0, SPL);                                                          \
+    late_row = idxq[R_];                                                                     \
+    idxq[R_] = fetch_row();                                                                  \
+    MR_STAMP(6)                                                                              \
+    /* fold the wave's 4 rows: reduce-scatter over the row groups */                         \
+    float t[NK / 2];                                                                         \
+    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = rs_level<32, true>(gme[i], gme[i + NK / 2], lane); \
+    float u[KP];                                                                             \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = rs_level<16, true>(t[i], t[i + KP], lane); \
+    const int par = s & 1;                                                                   \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
+    MR_STAMP(3)                                                                              \
+    lds_barrier();                 /* not __syncthreads: that would drain the ring */       \
+    MR_STAMP(4)                                                                              \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
+      float gs = gx[par][0][lane * KP + i];                                                  \
+      _Pragma("unroll") for (int k = 1; k < MQ_WAVES; ++k) gs += gx[par][k][lane * KP + i];  \
+      if (n0 + kj0 + i < N) momentum_step(po[i], bo[i], gs, first, mom, lr);                 \
+    }                                                                                        \
+    first = 0;                                                                               \
+    /* all-gather p back to NK clients per lane */                                           \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \
+    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
+    MR_STAMP(5)                                                                              \
+    ++s;                                                                                     \
+    if (pf_prog && (s & 3) == 0) mix_publish_progress(pf_prog, s);                           \
+  }
+  for (;;) {
+    MQ_STEP(0)
+    if constexpr (DEPTH > 1) MQ_STEP(1)
+    if constexpr (DEPTH > 2) MQ_STEP(2)
+  }
+#undef MQ_STEP
+#undef MQ_ISSUE
+  if (pf_prog) mix_publish_progress(pf_prog, total);   // releases the helpers
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int n = n0 + kj0 + i;
+      if (n < N) {
+        p[n] = po[i];
+        buf[n] = bo[i];
+      }
+    }
+    if (lane == 0 && total > 0) *first_flag = 0;
+#ifdef FS_MIX_STAMPS
+    if (lane < 6) reinterpret_cast<unsigned long long*>(buf + N + 8)[lane] = mr_acc[lane];
+#endif
+  }
+}
+
+static int quad_oob() {
+  const char* e = getenv("FS_MIX_QUAD_OOB");
+  return e && atoi(e) == 0 ? 0 : 1;
+}
+
+// default issue split: about 3/10 of the classes at the end of a step, the rest after the next
+// step's logits (r02s2j/k, config 2: 1.65 us per step unsplit, 1.42-1.47 split 3 or 5 without
+// helpers, 1.35-1.43 with 4 helpers; split 3 also keeps the (8, 10) instance in 242 VGPRs)
+template <int CL>
+constexpr int quad_split() { return (3 * CL + 9) / 10; }
+
+template <int NK, int CL, int SPL = quad_split<CL>()>
+static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                            int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                            int z_bytes, const MixPrefetch& pf) {
+  // ring: DEPTH x CL x NK floats per lane (<= 160), CL*NK/4 + 2 loads per step in the vmcnt window
+  constexpr int depth = (3 * CL * NK <= 160 && 3 * (CL * NK / 4 + 2) <= 63) ? 3 : 2;
+  const int blocks = pf.prog ? 8 * pf.h + 1 : 1;
+  hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z, y,
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, pf.h, pf.lead,
+                     quad_oob());
+}
+
+static bool quad_covers(int N, int C, int Bv, int nv, int epochs) {
+  const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
+  return Bv <= 16 && (N <= 64 ? C <= 16 : (N <= 128 && C <= 10)) && zb < ((int64_t)1 << 31) && (int64_t)epochs * nv < ((int64_t)1 << 31);
+}
+
+static bool mix_solve_quad(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
+                           int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
+                           const MixPrefetch& pf) {
+  if (!quad_covers(N, C, Bv, nv, epochs)) return false;
+  const int zb = (int)((int64_t)nv * C * mix_ldn(N) * 4);
+  const int nk = N <= 64 ? 4 : 8;
+#define MQ_CASE(NK_, CL_)                                                                                    \
+  if (nk == NK_ && C <= CL_) {                                                                               \
+    launch_mix_quad<NK_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);         \
+    return true;                                                                                             \
+  }
+  MQ_CASE(4, 2) MQ_CASE(4, 4) MQ_CASE(4, 8) MQ_CASE(4, 10) MQ_CASE(4, 16)
+  MQ_CASE(8, 2) MQ_CASE(8, 4) MQ_CASE(8, 8)
+  if (nk == 8 && C <= 10) {
+    // issue split (diagnostics, FS_MIX_QUAD_SPLIT): classes issued at the end of a step; the
+    // rest go out in the next step after its logits
+    const char* e = getenv("FS_MIX_QUAD_SPLIT");
+    const int spl = e ? atoi(e) : 3;
+    if (spl == 10) launch_mix_quad<8, 10, 10>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
+    else if (spl == 5) launch_mix_quad<8, 10, 5>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
+    else if (spl == 7) launch_mix_quad<8, 10, 7>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
+    else launch_mix_quad<8, 10>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
+    return true;
+  }
+#undef MQ_CASE
   return false;
 }
 
@@ -1565,13 +1905,40 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // and tests; a forced solver that does not cover the shape falls through to the next one)
   const char* pick = getenv("FS_MIX_SOLVER");
   const std::string want = pick ? pick : "auto";
-  // auto: the single-CU register solver where an instance covers the shape (no cross-CU
-  // exchange: ~1-2.5 us per step), else the multi-CU solver (~4-7 us per step, 7-11x the
-  // single-workgroup staged / global solvers at N = 200..1000, C = 10), else those.
+  const bool use_quad = (want == "auto" && !(N <= 16 && C <= 4) && quad_covers(N, C, Bv, n_val, epochs)) ||
+                        want == "quad";
+  MixPrefetch pf{nullptr, 0, 0};
+  {
+    // L2 prefetch helpers of the single-CU solvers: FS_MIX_PF_H helper workgroups (0 = off;
+    // default 4 for the quarter-wave solver, whose gather they speed up: r02s2k, 1.42-1.47 ->
+    // 1.35-1.43 us per step at config 2; 0 for the others, where they measured nothing),
+    // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
+    const char* eh = getenv("FS_MIX_PF_H");
+    const char* el = getenv("FS_MIX_PF_LEAD");
+    const int h = eh ? std::max(0, std::min(31, atoi(eh))) : (use_quad ? 4 : 0);
+    const int lead = el ? std::max(1, atoi(el)) : 16;
+    if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
+      pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
+      pf.h = h;
+      pf.lead = lead;
+      hipError_t e = hipMemsetAsync(pf.prog, 0, sizeof(unsigned), st0);
+      if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
+    }
+  }
+  // auto: one wave for N <= 16, C <= 4; the quarter-wave solver (+ L2 prefetch helpers) for
+  // N <= 64, C <= 16 or N <= 128, C <= 10; the register solvers where an instance covers the
+  // shape (no cross-CU exchange: ~1-2.5 us per step); else the multi-CU solver (~4-7 us per
+  // step, 7-11x the single-workgroup staged / global solvers at N = 200..1000, C = 10); else those.
   if (((want == "auto" && N <= 16 && C <= 4 && Bv <= 16) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
     hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
                        Bv, lr_p, momentum, d_p, d_buf, d_first);
     t_last_solver = 6;
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
+  if (use_quad &&
+      mix_solve_quad(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first, pf)) {
+    t_last_solver = 8;
     FS_LAUNCH_CHECK();
     return FS_OK;
   }
@@ -1584,7 +1951,8 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     return FS_OK;
   }
   if ((want == "auto" || want == "reg") &&
-      mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
+      mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first,
+                    pf)) {
     t_last_solver = 1;
     FS_LAUNCH_CHECK();
     return FS_OK;

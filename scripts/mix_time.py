@@ -51,7 +51,9 @@ mix.check_errors()
 print('  solver requested %s, ran %s' % (os.environ.get('FS_MIX_SOLVER', 'auto'),
                                          L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]), flush=True)
 if STAMPS:
-    acc = mix.buf[N + 8:N + 18].cpu().numpy().view(np.uint64)
-    names = ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update']
+    acc = mix.buf[N + 8:N + 20].cpu().numpy().view(np.uint64)
+    names = (['wait+logits', 'rs+softmax+grad', 'fold', 'barrier', 'update+gather', 'issue']
+             if os.environ.get('FS_MIX_SOLVER') == 'quad' else
+             ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update'])
     print('wave-0 s_memtime ticks per step (last call): ' +
           ', '.join('%s %.0f' % (nm, a / steps) for nm, a in zip(names, acc)), flush=True)

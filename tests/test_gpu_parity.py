@@ -343,8 +343,9 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
-@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'wave'), (16, 4, 16, 'wave'), (17, 4, 16, 'reg'),
-                                           (10, 5, 16, 'reg'), (100, 10, 16, 'reg'), (200, 4, 16, 'reg2'),
+@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'wave'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
+                                           (10, 5, 16, 'quad'), (100, 10, 16, 'quad'), (64, 16, 16, 'quad'),
+                                           (37, 20, 16, 'reg'), (129, 3, 16, 'reg2'), (200, 4, 16, 'reg2'),
                                            (1000, 10, 16, 'mc'), (23, 5, 24, 'staged')])
 def test_mix_solve_auto_choice(amd, N, C, Bv, solver):
     """The solver fs_mix_solve picks by shape."""
@@ -406,6 +407,78 @@ def test_mix_solve_rows(amd, monkeypatch, N, C, nv, Bv, rw):
     monkeypatch.setenv('FS_MIX_ROWS_RW', str(rw))
     test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.1 if N == 200 else 0.5)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'rows'
+
+
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (100, 10, 517, 16),     # config 2 shape: NK = 8, CL = 10
+    (10, 2, 203, 16),       # config 1 shape: NK = 4, CL = 2
+    (16, 4, 77, 16),        # ragged last batch
+    (5, 3, 40, 7),          # Bv = 7: idle row groups, N not a multiple of 4
+    (1, 2, 33, 16),         # one client
+    (60, 8, 33, 9),         # NK = 4, CL = 8, 9-row batches
+    (64, 7, 130, 16),       # N = 64: every lane's clients real
+    (37, 16, 90, 16),       # C = 16: every class slot real, 2-deep ring
+    (128, 10, 77, 8),       # N = 128 (NK = 8 exactly), Bv = 8
+    (65, 9, 211, 16),       # NK = 8, C = 9 < CL = 10 (class padding), ragged chunks
+])
+def test_mix_solve_quad(amd, monkeypatch, N, C, nv, Bv):
+    """fs_mix_solve's quarter-wave solver (4 batch rows per wave, 16 lanes per row; default
+    issue split and L2 prefetch helpers) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
+    test_mix_solve_variants(amd, N, C, nv, Bv)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
+
+
+@pytest.mark.parametrize('split', [5, 7, 10])
+@pytest.mark.parametrize('oob', [0, 1])
+def test_mix_solve_quad_issue_forms(amd, monkeypatch, split, oob):
+    """The quarter-wave solver's other load-issue splits (classes issued at the end of a step,
+    the rest after the next step's logits) and padding-chunk forms at config 2's shape."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
+    monkeypatch.setenv('FS_MIX_QUAD_SPLIT', str(split))
+    monkeypatch.setenv('FS_MIX_QUAD_OOB', str(oob))
+    test_mix_solve_variants(amd, 100, 10, 517, 16)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
+
+
+@pytest.mark.parametrize('h,lead', [(1, 1), (3, 16), (7, 64)])
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (100, 10, 517, 16),     # config 2 shape
+    (64, 7, 130, 16),       # NK = 1
+    (129, 3, 77, 8),        # NK = 4, Bv < 16: idle waves in the helpers too, ragged last batch
+])
+@pytest.mark.parametrize('solver', ['reg', 'quad'])
+def test_mix_solve_prefetch_helpers(amd, monkeypatch, N, C, nv, Bv, h, lead, solver):
+    """The single-CU solvers with L2 prefetch helper workgroups (FS_MIX_PF_H): the helpers
+    only load, so p and the momentum buffer are bitwise those of the solver alone, and match
+    the oracle's p-SGD."""
+    if solver == 'quad' and N > 128:
+        pytest.skip('the quarter-wave solver covers N <= 128')
+    monkeypatch.setenv('FS_MIX_SOLVER', solver)
+    rs = np.random.RandomState(N + nv)
+    D = 64
+    Xv = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
+    yv = torch.from_numpy(rs.randint(0, C, size=nv).astype(np.int64))
+    p0 = torch.from_numpy(rs.dirichlet(np.ones(N)).astype(np.float32))
+    Ws = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.5).astype(np.float32))
+    dev = torch.device('cuda')
+    out = []
+    for helpers in (0, h):
+        monkeypatch.setenv('FS_MIX_PF_H', str(helpers))
+        monkeypatch.setenv('FS_MIX_PF_LEAD', str(lead))
+        mix = amd.engine.Mixture(Xv, yv, D, C, N, Bv, p0, dev)
+        Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+        Wd[:, :, :D] = Ws
+        for rnd in range(2):
+            torch.manual_seed(90 + rnd)
+            mix.solve(Wd, amd.rng.draw_pass_seeds(3), 0.5)
+        torch.cuda.synchronize()
+        mix.check_errors()
+        assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
+        out.append((mix.p.cpu().clone(), mix.buf.cpu().clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    monkeypatch.setenv('FS_MIX_PF_H', str(h))
+    test_mix_solve_variants(amd, N, C, nv, Bv)
 
 
 def test_mix_solve_rows_timeout_raises(amd, monkeypatch):
