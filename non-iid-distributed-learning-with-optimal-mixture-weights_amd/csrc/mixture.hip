@@ -610,9 +610,9 @@ static void launch_mix_reg(hipStream_t st, const float* Z, const int32_t* y, con
                            int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
                            const MixPrefetch& pf) {
   constexpr int depth = 3 * (CL + 2) <= 63 ? 3 : 2;   // CL + 2 loads per step stay in the vmcnt window
-  const int blocks = pf.prog ? 8 * pf.h + 1 : 1;
+  const int blocks = pf.prog ? 8 * std::min(pf.h, 31) + 1 : 1;
   hipLaunchKernelGGL((mix_solve_reg_kernel<NK, CP, CL, depth>), dim3(blocks), dim3(MR_WAVES * 64), 0, st, Z, y,
-                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, pf.prog, pf.h, pf.lead);
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, pf.prog, std::min(pf.h, 31), pf.lead);
 }
 
 // register-resident solver for (N, C, Bv) if an instance covers it
@@ -1390,9 +1390,9 @@ static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, co
                             int z_bytes, const MixPrefetch& pf) {
   // ring: DEPTH x CL x NK floats per lane (<= 160), CL*NK/4 + 2 loads per step in the vmcnt window
   constexpr int depth = (3 * CL * NK <= 160 && 3 * (CL * NK / 4 + 2) <= 63) ? 3 : 2;
-  const int blocks = pf.prog ? 8 * pf.h + 1 : 1;
+  const int blocks = pf.prog ? 8 * std::min(pf.h, 31) + 1 : 1;   // helpers: the solver's XCD only
   hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z, y,
-                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, pf.h, pf.lead,
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31), pf.lead,
                      quad_oob());
 }
 
@@ -1613,10 +1613,17 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
                                                                  int* __restrict__ first_flag,
                                                                  unsigned long long* __restrict__ xbuf,
                                                                  unsigned* __restrict__ err, int K,
-                                                                 unsigned spin_limit) {
+                                                                 unsigned spin_limit, unsigned* __restrict__ pf_prog,
+                                                                 int pf_h, int pf_lead) {
   static_assert(S == 8 || S == 16 || S == 32 || S == 64, "slice width");
   static_assert(HOPS == 1 || HOPS == 2, "exchange form");
-  if (blockIdx.x % MC_XCDS) return;
+  if (blockIdx.x % MC_XCDS) {
+    // the other XCDs' blocks: the first pf_h prefetch the Z rows of the steps ahead into the
+    // Infinity Cache (shared by all XCDs; their own L2s are of no use to the solver's XCD)
+    const int hidx = (int)blockIdx.x - (int)blockIdx.x / MC_XCDS - 1;
+    if (pf_prog && hidx < pf_h) mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, hidx, pf_h, pf_lead, pf_prog);
+    return;
+  }
   constexpr int LPV = 64 / S;                      // lanes per value after the reduce-scatter
   __shared__ __attribute__((aligned(16))) float ps[S];
   __shared__ float gp[MC_THREADS / 64][S];
@@ -1787,7 +1794,9 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
     for (int i = 0; i < S / 4; ++i) zc[i] = zn[i];
     yc = yn;
     vnext = vn2;
+    if (pf_prog && k == 0 && ((st + 1) & 3) == 0) mix_publish_progress(pf_prog, st + 1);
   }
+  if (pf_prog && k == 0) mix_publish_progress(pf_prog, total);   // releases the helpers
   if (t < S && myn < N) {
     p[myn] = dead ? __int_as_float(0x7fc00000) : pr;
     buf[myn] = br;
@@ -1832,7 +1841,7 @@ static bool mc_covers(int N, int C, int Bv) { return mc_slice(N) != 0 && C <= 16
 
 static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
                         int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first, void* d_ws,
-                        int64_t ws_bytes) {
+                        int64_t ws_bytes, MixPrefetch pf) {
   if (!mc_covers(N, C, Bv)) return 1;            // not covered
   const int S = mc_slice(N);
   const int K = (mix_ldn(N) + S - 1) / S;
@@ -1849,12 +1858,13 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   // Z-slice issue point (FS_MIX_MC_ZAT=0|1|2 for diagnostics): after the exchange by default --
   // r02i, us per step, (hops, ZAT) = (1, 0) / (2, 0) / (2, 1) / (2, 2): N = 1000, C = 10, K = 32:
   // 6.61 / 6.03 / 5.45 / 5.44; N = 300, C = 4, K = 19: 4.33 / 4.34 / 4.08 / 3.38
+  if (pf.prog) pf.h = std::min(pf.h, (MC_XCDS - 1) * K);   // helpers: the grid's other-XCD blocks
   const char* zenv = getenv("FS_MIX_MC_ZAT");
   const int zat = zenv ? std::min(2, std::max(0, atoi(zenv))) : 2;
 #define MC_CASE(S_, H_, Z_)                                                                                   \
   if (S == S_ && hops == H_ && zat == Z_)                                                                     \
     hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_, Z_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, \
-                       mom, p, buf, first, ws, err, K, spin_limit);
+                       mom, p, buf, first, ws, err, K, spin_limit, pf.prog, pf.h, pf.lead);
 #define MC_CASES(Z_) \
   MC_CASE(8, 1, Z_) MC_CASE(16, 1, Z_) MC_CASE(32, 1, Z_) MC_CASE(64, 1, Z_) \
   MC_CASE(8, 2, Z_) MC_CASE(16, 2, Z_) MC_CASE(32, 2, Z_) MC_CASE(64, 2, Z_)
@@ -1915,7 +1925,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
     const char* eh = getenv("FS_MIX_PF_H");
     const char* el = getenv("FS_MIX_PF_LEAD");
-    const int h = eh ? std::max(0, std::min(31, atoi(eh))) : (use_quad ? 4 : 0);
+    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : 0);
     const int lead = el ? std::max(1, atoi(el)) : 16;
     if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
       pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
@@ -1969,7 +1979,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   }
   if (want == "auto" || want == "mc") {
     const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
-                                d_first, d_ws, ws_bytes);
+                                d_first, d_ws, ws_bytes, pf);
     if (rc < 0) return rc;
     if (rc == 0) {
       t_last_solver = 2;
