@@ -7,7 +7,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 TAG=${1:-s2}; shift
 O=gpurun_out/$TAG; mkdir -p $O
-for c in "${@:-c2 c2_fedamw}"; do
+[ $# -gt 0 ] || set -- c2 c2_fedamw
+for c in "$@"; do
   case $c in
     c2) bash scripts/pmc_capture.sh c2 "--config 2 --steps 3 --warmup 1 --no-fedamw-leg" "local_train" || exit 1 ;;
     c2_fedamw) bash scripts/pmc_capture.sh c2_fedamw "--config 2 --algo fedamw --steps 1 --warmup 1" "mix_solve" || exit 1 ;;
