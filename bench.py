@@ -156,7 +156,7 @@ def pool_validation(d, ws, dev):
 
 
 def phase_ms(events, name):
-    v = [a.elapsed_time(b) for n, a, b in events if n == name]
+    v = [a.elapsed_time(b) for n, a, b in (events or []) if n == name]
     return float(np.mean(v)) if v else None
 
 
@@ -244,17 +244,24 @@ def main():
     for _ in range(args.warmup):
         fed.round()
     torch.cuda.synchronize()
-    fed.events = []
+    fed.events = None if os.environ.get('FS_BENCH_NO_EVENTS') == '1' else []   # (diagnostic A/B)
     if ws > 1:
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_t = []
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         fed.round()
+        host_t.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     if ws > 1:
         tdist.barrier()
     el = time.perf_counter() - t0
+    if os.environ.get('FS_BENCH_HOST_TIMES') == '1':     # (diagnostic: host enqueue time per round)
+        print('host us per round() call: mean %.1f min %.1f max %.1f; wall per round %.1f'
+              % (1e6 * np.mean(host_t), 1e6 * np.min(host_t), 1e6 * np.max(host_t), 1e6 * el / args.steps),
+              file=sys.stderr, flush=True)
     if ws > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -263,7 +270,7 @@ def main():
     tr, tl, ta = fed.results()
     n_rows = int(fed.feats.rows)
     alg_bytes = 4.0 * E * n_rows * args.D + 8.0 * E * n_rows + 8.0 * N_loc * args.C * args.D
-    achieved = alg_bytes / (lt_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (lt_ms * 1e-3) / 1e9 if lt_ms else float('nan')
     tag = 'c%d%s' % (args.config, '' if args.algo == PRESETS[args.config]['algo'] else '_' + args.algo)
     traffic, tnote = (None, 'custom workload') if args.custom else load_traffic(tag)
     total = N_loc * ws

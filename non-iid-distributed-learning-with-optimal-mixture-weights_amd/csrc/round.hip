@@ -31,6 +31,9 @@
 #include <thread>
 #include <vector>
 
+#include <chrono>
+#include <cstdio>
+
 #include "common.h"
 #include "mt_replay.h"
 
@@ -112,8 +115,17 @@ struct fs_plan {
   int64_t perm_len = 0;                // E * rows
   int32_t* h_perm[2] = {nullptr, nullptr};   // pinned (host replay)
   int32_t* d_perm[2] = {nullptr, nullptr};
-  int64_t* h_seed[2] = {nullptr, nullptr};   // pinned (device replay)
-  int64_t* d_seed[2] = {nullptr, nullptr};
+  // device replay: a ring of SEED_SLOTS pinned seed buffers, each freed by its own event, so the
+  // host never waits on the shuffle of the previous round before enqueuing the next (with two
+  // slots that wait held the host ~330 us per round at config 2 and left the GPU idle between
+  // rounds -- r02s2t)
+  static constexpr int SEED_SLOTS = 4;
+  int64_t* h_seed[SEED_SLOTS] = {};             // pinned, coherent
+  int64_t* d_seed[SEED_SLOTS] = {};
+  int64_t* h_seed_dev[SEED_SLOTS] = {};         // device view of h_seed (zero-copy seeds)
+  hipEvent_t seed_read[SEED_SLOTS] = {};
+  bool seed_pending[SEED_SLOTS] = {};
+  bool seed_copy = false;                         // FS_SEED_COPY=1: upload the seeds (hipMemcpyAsync)
   int64_t* d_pass = nullptr;                 // [2][P]: rows, offset of every pass (device replay)
   int64_t max_n = 0;
   hipStream_t copy = nullptr;
@@ -183,10 +195,13 @@ extern "C" int fs_plan_destroy(fs_plan* p) {
   for (int s = 0; s < 2; ++s) {
     if (p->h_perm[s]) (void)hipHostFree(p->h_perm[s]);
     if (p->d_perm[s]) (void)hipFree(p->d_perm[s]);
-    if (p->h_seed[s]) (void)hipHostFree(p->h_seed[s]);
-    if (p->d_seed[s]) (void)hipFree(p->d_seed[s]);
     if (p->uploaded[s]) (void)hipEventDestroy(p->uploaded[s]);
     if (p->consumed[s]) (void)hipEventDestroy(p->consumed[s]);
+  }
+  for (int s = 0; s < fs_plan::SEED_SLOTS; ++s) {
+    if (p->h_seed[s]) (void)hipHostFree(p->h_seed[s]);
+    if (p->d_seed[s]) (void)hipFree(p->d_seed[s]);
+    if (p->seed_read[s]) (void)hipEventDestroy(p->seed_read[s]);
   }
   if (p->d_pass) (void)hipFree(p->d_pass);
   if (p->copy) (void)hipStreamDestroy(p->copy);
@@ -221,16 +236,31 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
   for (int64_t v : p->n) p->max_n = std::max(p->max_n, v);
   hipError_t e = hipSuccess;
   for (int s = 0; s < 2 && e == hipSuccess; ++s) {
-    if (d.shuffle_device) {
-      e = hipHostMalloc(reinterpret_cast<void**>(&p->h_seed[s]), sizeof(int64_t) * std::max<int64_t>(1, P),
-                        hipHostMallocDefault);
-      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_seed[s]), sizeof(int64_t) * std::max<int64_t>(1, P));
-    } else {
+    if (!d.shuffle_device) {
       e = hipHostMalloc(reinterpret_cast<void**>(&p->h_perm[s]), sizeof(int32_t) * p->perm_len, hipHostMallocDefault);
     }
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_perm[s]), sizeof(int32_t) * p->perm_len);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->uploaded[s], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->consumed[s], hipEventDisableTiming);
+    // ordering-only events: no timestamps and no system-scope release when they complete (the
+    // waits are device-side, and the host only needs the seed upload's completion, not the
+    // visibility of device writes) -- FS_EVENT_FENCE=1 restores the default release
+    const char* ef = getenv("FS_EVENT_FENCE");
+    const unsigned evf = hipEventDisableTiming | ((ef && atoi(ef) == 1) ? 0u : (unsigned)hipEventDisableSystemFence);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->uploaded[s], evf);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->consumed[s], evf);
+  }
+  if (d.shuffle_device) {
+    // the seeds stay in pinned, coherent host memory that the shuffle kernel reads directly
+    // (FS_SEED_COPY=1: upload them with hipMemcpyAsync instead)
+    const char* sc = getenv("FS_SEED_COPY");
+    p->seed_copy = sc && atoi(sc) == 1;
+    for (int k = 0; k < fs_plan::SEED_SLOTS && e == hipSuccess; ++k) {
+      e = hipHostMalloc(reinterpret_cast<void**>(&p->h_seed[k]), sizeof(int64_t) * std::max<int64_t>(1, P),
+                        p->seed_copy ? hipHostMallocDefault : (hipHostMallocMapped | hipHostMallocCoherent));
+      if (e == hipSuccess && !p->seed_copy)
+        e = hipHostGetDevicePointer(reinterpret_cast<void**>(&p->h_seed_dev[k]), p->h_seed[k], 0);
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_seed[k]), sizeof(int64_t) * std::max<int64_t>(1, P));
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&p->seed_read[k], hipEventDisableTiming | hipEventDisableSystemFence);
+    }
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking);
   if (e == hipSuccess && d.shuffle_device && P > 0) {
@@ -260,19 +290,43 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
 }
 
 // Device replay: upload the seeds and launch fs_randperm_device on the side stream.
+static double now_us() {
+  return 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   const int s = t & 1;
   const int64_t P = (int64_t)p->n.size();
-  if (p->up_pending[s]) FS_HIP(hipEventSynchronize(p->uploaded[s]), "fs_plan_shuffle");   // pinned seeds free
-  std::memcpy(p->h_seed[s], h_seeds, sizeof(int64_t) * P);
+  static const bool trace = getenv("FS_PLAN_TRACE") && atoi(getenv("FS_PLAN_TRACE")) == 1;   // diagnostics
+  double t0 = trace ? now_us() : 0.0, t1 = 0.0, t2 = 0.0;
+  const int k = t % fs_plan::SEED_SLOTS;
+  long polls = 0;
+  if (p->seed_pending[k]) {                        // pinned seeds free
+    // poll rather than hipEventSynchronize (diagnostics: FS_PLAN_TRACE reports the polls)
+    hipError_t q;
+    while ((q = hipEventQuery(p->seed_read[k])) == hipErrorNotReady) ++polls;
+    FS_HIP(q, "fs_plan_shuffle");
+  }
+  if (trace) t1 = now_us();
+  std::memcpy(p->h_seed[k], h_seeds, sizeof(int64_t) * P);
   if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
   // optionally also behind the latest local training (the other slot's consumer)
   if (p->d.shuffle_after_train && p->cons_recorded[s ^ 1])
     FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s ^ 1], 0), "fs_plan_shuffle");
-  FS_HIP(hipMemcpyAsync(p->d_seed[s], p->h_seed[s], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
-         "fs_plan_shuffle");
-  const int rc = fs_randperm_device(p->d_seed[s], p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], p->copy);
+  if (trace) {
+    t2 = now_us();
+    fprintf(stderr, "fs_plan_shuffle t=%d: seed-slot wait %.1f us (%ld polls), stream wait %.1f us\n", t, t1 - t0,
+            polls, t2 - t1);
+  }
+  if (p->seed_copy)
+    FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
+           "fs_plan_shuffle");
+  const int64_t* seeds = p->seed_copy ? p->d_seed[k] : p->h_seed_dev[k];
+  const int rc = fs_randperm_device(seeds, p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], p->copy);
   if (rc != FS_OK) return rc;
+  FS_HIP(hipEventRecord(p->seed_read[k], p->copy), "fs_plan_shuffle");
+  p->seed_pending[k] = true;
   FS_HIP(hipEventRecord(p->uploaded[s], p->copy), "fs_plan_shuffle");
   p->up_pending[s] = true;
   p->slot_round[s] = t;
