@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 6
+#define FS_ABI_VERSION 7
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -276,6 +276,16 @@ int fs_plan_create(const fs_plan_desc* desc, fs_plan** out);
 int fs_plan_destroy(fs_plan* plan);
 int fs_plan_shuffle(fs_plan* plan, const int64_t* h_seeds, int t);
 int fs_plan_round(fs_plan* plan, int t, float lr, int phases, const float* d_p_override, void* stream);
+/* ABI 7 (device replay only; call before the first fs_plan_shuffle): generate the shuffles of
+ * `rounds` consecutive rounds (a chunk: rounds cK .. cK+K-1) with ONE fs_randperm_device launch
+ * into one of two chunk slots.  fs_plan_shuffle then only collects round t's seeds and launches
+ * when the chunk's last round arrives (a partly collected chunk is launched by the first
+ * fs_plan_round that needs it); the local training waits for its slot, and releases it, once
+ * per chunk instead of once per round -- no cross-stream wait between the rounds of a chunk.
+ * Rounds must be prepared in order; prepare chunk c+1 while chunk c runs. */
+int fs_plan_set_shuffle_chunk(fs_plan* plan, int rounds);
+/* ABI 7: launch a partly collected chunk now (after preparing a run's last round). */
+int fs_plan_shuffle_flush(fs_plan* plan);
 
 #ifdef __cplusplus
 }

@@ -49,10 +49,12 @@ _SIGS = {
     'fs_plan_destroy': (C.c_int, [C.c_void_p]),
     'fs_plan_shuffle': (C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
     'fs_plan_round': (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p]),
+    'fs_plan_set_shuffle_chunk': (C.c_int, [C.c_void_p, C.c_int]),
+    'fs_plan_shuffle_flush': (C.c_int, [C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)

@@ -42,7 +42,16 @@ struct LTParams {
   const float* W_start;
   float* W_out;
   double* loss;
+  int64_t max_client_steps = 0;   // host bound on E * ceil(n_j / B) over the clients (0: unknown)
 };
+
+// fs_local_train with a host bound on the steps of any client (the round plan knows the
+// client sizes; with the bound the split kernel tags its hand-offs by launch generation
+// instead of clearing its exchange buffer before every launch)
+int local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
+                const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E, float lr, float mu,
+                int prox, float lam, int reg, int chained, const float* d_W_start, float* d_W_out, double* d_loss,
+                int G, void* d_ws, int64_t ws_bytes, hipStream_t st, int64_t max_client_steps);
 
 // split-client launcher (local_train_split.hip): G workgroups per client
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);

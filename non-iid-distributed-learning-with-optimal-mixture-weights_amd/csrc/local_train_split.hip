@@ -31,7 +31,9 @@
 // every spin is bounded and a timeout is reported through the workspace error word.
 // Hand-off tags are the group's step counter + 1 (32 bits): the exchange buffer is zeroed by
 // the launcher before every launch.
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "common.h"
 #include "lanes.h"
@@ -65,6 +67,7 @@ struct SplitWS {
   unsigned long long* xbuf;            // [ngroups][2][G][SZ] published partials: {tag, value} granules
   unsigned long long* stamps;          // [grid][16] diagnostic build only
   int SZ;                              // granules per (group, parity, slice)
+  unsigned tag_base;                   // launch generation << 20 (0: the buffer was zeroed for this launch)
   int ngroups;
   unsigned spin_limit;                 // 0: test knob -- report a timeout at the first hand-off
 };
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       const int e = st / nbat, s = st - e * nbat;
       const int b0 = s * B, bc = min(B, n - b0);
       const int par = gs & 1;
-      const unsigned tag32 = gs + 1u;
+      const unsigned tag32 = X.tag_base + gs + 1u;
       if (w == 0 && lg == 0)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) lab[par][rt * 16 + l16] = lb[rt];
@@ -739,9 +742,30 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
 #ifdef FS_STAMPS
   X.stamps = reinterpret_cast<unsigned long long*>(base + xbytes);
 #endif
-  // hand-off tags restart at 1 every launch: clear the exchange granules
-  hipError_t e = hipMemsetAsync(base, 0, (size_t)xbytes, st);
-  if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
+  // Hand-off tags: (launch generation << 20) + group step + 1, the generation counted per
+  // workspace on the host, so a granule left by an earlier launch never carries a tag this
+  // launch waits for and the exchange buffer needs no clearing per launch.  It is cleared
+  // when a workspace is first seen, every 4095 launches (the generation wraps) and for a
+  // launch whose groups may run 2^20 - 1 steps or more (then the generation is 0: tags are
+  // the step + 1 alone, as after any clearing).
+  unsigned gen = 0;
+  {
+    static std::mutex gm;
+    static std::unordered_map<const void*, unsigned> gens;
+    // (groups walk clients in snake order: at most ceil(N / ng) each; chained: all N)
+    const int64_t groups_clients = P.chained ? P.N : (P.N + ng - 1) / ng;
+    const bool long_launch = P.max_client_steps <= 0 || P.max_client_steps * groups_clients >= (1 << 20) - 1;
+    std::lock_guard<std::mutex> lk(gm);
+    auto it = gens.find(ws);
+    const unsigned prev = it == gens.end() ? 0u : it->second;
+    gen = (long_launch || prev >= 4095u) ? 0u : prev + 1u;
+    gens[ws] = gen;
+  }
+  X.tag_base = gen << 20;
+  if (gen <= 1) {                      // first use, wrap or long launch: clear the granules
+    hipError_t e = hipMemsetAsync(base, 0, (size_t)xbytes, st);
+    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
+  }
   const size_t lds = split_dyn_lds(RT, NT, G);
   const int grid = P.chained ? 8 * G : ng * G;
 #define FS_SPLIT_CASE(rt, g) \

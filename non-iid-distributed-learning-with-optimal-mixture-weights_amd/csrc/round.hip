@@ -128,12 +128,23 @@ struct fs_plan {
   bool seed_copy = false;                         // FS_SEED_COPY=1: upload the seeds (hipMemcpyAsync)
   int64_t* d_pass = nullptr;                 // [2][P]: rows, offset of every pass (device replay)
   int64_t max_n = 0;
+  int64_t max_client_steps = 0;       // E * ceil(max_j n_j / B)
   hipStream_t copy = nullptr;
   hipEvent_t uploaded[2] = {nullptr, nullptr};
   hipEvent_t consumed[2] = {nullptr, nullptr};
   bool up_pending[2] = {false, false};
   bool cons_recorded[2] = {false, false};
   int slot_round[2] = {-1, -1};       // round whose shuffles slot s holds (set by the coordinator)
+  // chunked device replay (fs_plan_set_shuffle_chunk, K > 1): slot s holds the shuffles of
+  // the K rounds of chunk c (rounds cK .. cK+K-1), generated by ONE launch; the local
+  // training waits for the slot once per chunk and records its release once per chunk, so
+  // consecutive rounds of a chunk run back to back with no cross-stream wait between them
+  int chunk = 1;
+  int64_t* d_pass_chunk = nullptr;    // [2][K*P]: rows, offset of every pass of a chunk
+  int slot_chunk[2] = {-1, -1};       // chunk whose shuffles slot s holds (launched)
+  int slot_nrounds[2] = {0, 0};       // rounds of that chunk generated
+  int slot_waited[2] = {-1, -1};      // chunk the compute stream last waited for in slot s
+  int fill_chunk = -1, fill_rounds = 0;   // chunk whose seeds are being collected, rounds so far
   int job_status = FS_OK;
   std::string job_error;
   fs::Pool* pool = nullptr;
@@ -204,6 +215,7 @@ extern "C" int fs_plan_destroy(fs_plan* p) {
     if (p->seed_read[s]) (void)hipEventDestroy(p->seed_read[s]);
   }
   if (p->d_pass) (void)hipFree(p->d_pass);
+  if (p->d_pass_chunk) (void)hipFree(p->d_pass_chunk);
   if (p->copy) (void)hipStreamDestroy(p->copy);
   delete p->pool;
   delete p;
@@ -234,6 +246,11 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
   p->perm_len = std::max<int64_t>(1, (int64_t)d.E * rows);
   const int64_t P = (int64_t)p->n.size();
   for (int64_t v : p->n) p->max_n = std::max(p->max_n, v);
+  {
+    int64_t mx = 0;
+    for (int j = 0; j < d.N; ++j) mx = std::max(mx, d.h_n[j]);
+    p->max_client_steps = std::max<int64_t>(1, (int64_t)d.E * ((mx + d.B - 1) / std::max(1, d.B)));
+  }
   hipError_t e = hipSuccess;
   for (int s = 0; s < 2 && e == hipSuccess; ++s) {
     if (!d.shuffle_device) {
@@ -301,13 +318,7 @@ static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   static const bool trace = getenv("FS_PLAN_TRACE") && atoi(getenv("FS_PLAN_TRACE")) == 1;   // diagnostics
   double t0 = trace ? now_us() : 0.0, t1 = 0.0, t2 = 0.0;
   const int k = t % fs_plan::SEED_SLOTS;
-  long polls = 0;
-  if (p->seed_pending[k]) {                        // pinned seeds free
-    // poll rather than hipEventSynchronize (diagnostics: FS_PLAN_TRACE reports the polls)
-    hipError_t q;
-    while ((q = hipEventQuery(p->seed_read[k])) == hipErrorNotReady) ++polls;
-    FS_HIP(q, "fs_plan_shuffle");
-  }
+  if (p->seed_pending[k]) FS_HIP(hipEventSynchronize(p->seed_read[k]), "fs_plan_shuffle");   // pinned seeds free
   if (trace) t1 = now_us();
   std::memcpy(p->h_seed[k], h_seeds, sizeof(int64_t) * P);
   if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
@@ -316,8 +327,7 @@ static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
     FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s ^ 1], 0), "fs_plan_shuffle");
   if (trace) {
     t2 = now_us();
-    fprintf(stderr, "fs_plan_shuffle t=%d: seed-slot wait %.1f us (%ld polls), stream wait %.1f us\n", t, t1 - t0,
-            polls, t2 - t1);
+    fprintf(stderr, "fs_plan_shuffle t=%d: seed-slot wait %.1f us, stream wait %.1f us\n", t, t1 - t0, t2 - t1);
   }
   if (p->seed_copy)
     FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
@@ -333,11 +343,108 @@ static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   return FS_OK;
 }
 
+// Chunked device replay: the seeds of rounds cK .. cK+K-1 are collected in one pinned seed
+// slot; one fs_randperm_device launch over all K*P passes fills shuffle slot c & 1.
+extern "C" int fs_plan_set_shuffle_chunk(fs_plan* p, int rounds) {
+  FS_REQUIRE(p && rounds >= 1 && rounds <= 64, "bad arguments");
+  FS_REQUIRE(p->d.shuffle_device, "fs_plan_set_shuffle_chunk: device replay only");
+  FS_REQUIRE(!p->seed_pending[0] && p->slot_round[0] < 0 && p->slot_round[1] < 0 && p->slot_chunk[0] < 0 &&
+                 p->fill_chunk < 0,
+             "fs_plan_set_shuffle_chunk: set before the first shuffle");
+  if (rounds == p->chunk) return FS_OK;
+  const int64_t P = (int64_t)p->n.size();
+  const int64_t KP = std::max<int64_t>(1, (int64_t)rounds * P);
+  for (int s = 0; s < 2; ++s) {
+    FS_HIP(hipFree(p->d_perm[s]), "fs_plan_set_shuffle_chunk");
+    p->d_perm[s] = nullptr;
+    FS_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_perm[s]), sizeof(int32_t) * p->perm_len * rounds),
+           "fs_plan_set_shuffle_chunk");
+  }
+  for (int k = 0; k < fs_plan::SEED_SLOTS; ++k) {
+    FS_HIP(hipHostFree(p->h_seed[k]), "fs_plan_set_shuffle_chunk");
+    FS_HIP(hipFree(p->d_seed[k]), "fs_plan_set_shuffle_chunk");
+    p->h_seed[k] = nullptr;
+    p->d_seed[k] = nullptr;
+    FS_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->h_seed[k]), sizeof(int64_t) * KP,
+                         p->seed_copy ? hipHostMallocDefault : (hipHostMallocMapped | hipHostMallocCoherent)),
+           "fs_plan_set_shuffle_chunk");
+    if (!p->seed_copy)
+      FS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->h_seed_dev[k]), p->h_seed[k], 0),
+             "fs_plan_set_shuffle_chunk");
+    FS_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_seed[k]), sizeof(int64_t) * KP), "fs_plan_set_shuffle_chunk");
+  }
+  if (p->d_pass_chunk) FS_HIP(hipFree(p->d_pass_chunk), "fs_plan_set_shuffle_chunk");
+  p->d_pass_chunk = nullptr;
+  if (P > 0) {
+    std::vector<int64_t> h(2 * KP);
+    for (int r = 0; r < rounds; ++r)
+      for (int64_t i = 0; i < P; ++i) {
+        h[r * P + i] = p->n[i];
+        h[KP + r * P + i] = p->off[i] + (int64_t)r * p->perm_len;
+      }
+    FS_HIP(hipMalloc(reinterpret_cast<void**>(&p->d_pass_chunk), sizeof(int64_t) * 2 * KP),
+           "fs_plan_set_shuffle_chunk");
+    FS_HIP(hipMemcpy(p->d_pass_chunk, h.data(), sizeof(int64_t) * 2 * KP, hipMemcpyHostToDevice),
+           "fs_plan_set_shuffle_chunk");
+  }
+  p->chunk = rounds;
+  return FS_OK;
+}
+
+// launch the shuffles of the collected rounds of chunk p->fill_chunk into slot (chunk & 1)
+static int launch_chunk(fs_plan* p) {
+  const int c = p->fill_chunk, nr = p->fill_rounds, K = p->chunk;
+  const int s = c & 1, k = c % fs_plan::SEED_SLOTS;
+  const int64_t P = (int64_t)p->n.size(), KP = std::max<int64_t>(1, (int64_t)K * P);
+  // the slot's previous chunk (c - 2) released it after its last local training
+  if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
+  if (P > 0) {
+    if (p->seed_copy)
+      FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * nr * P, hipMemcpyHostToDevice, p->copy),
+             "fs_plan_shuffle");
+    const int64_t* seeds = p->seed_copy ? p->d_seed[k] : p->h_seed_dev[k];
+    const int rc = fs_randperm_device(seeds, p->d_pass_chunk, p->d_pass_chunk + KP, nr * P, p->max_n, p->d_perm[s],
+                                      p->copy);
+    if (rc != FS_OK) return rc;
+  }
+  FS_HIP(hipEventRecord(p->seed_read[k], p->copy), "fs_plan_shuffle");
+  p->seed_pending[k] = true;
+  FS_HIP(hipEventRecord(p->uploaded[s], p->copy), "fs_plan_shuffle");
+  p->up_pending[s] = true;
+  p->slot_chunk[s] = c;
+  p->slot_nrounds[s] = nr;
+  p->fill_chunk = -1;
+  p->fill_rounds = 0;
+  return FS_OK;
+}
+
+static int chunk_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
+  const int K = p->chunk, c = t / K, r = t % K;
+  const int64_t P = (int64_t)p->n.size();
+  FS_REQUIRE(r == (p->fill_chunk == c ? p->fill_rounds : 0) && (r > 0 || p->fill_chunk < 0),
+             "rounds must be prepared in order");
+  if (r == 0) {
+    const int k = c % fs_plan::SEED_SLOTS;
+    if (p->seed_pending[k]) FS_HIP(hipEventSynchronize(p->seed_read[k]), "fs_plan_shuffle");   // seed slot free
+    p->fill_chunk = c;
+    p->fill_rounds = 0;
+  }
+  std::memcpy(p->h_seed[c % fs_plan::SEED_SLOTS] + (int64_t)r * P, h_seeds, sizeof(int64_t) * P);
+  ++p->fill_rounds;
+  return r == K - 1 ? launch_chunk(p) : FS_OK;
+}
+
+extern "C" int fs_plan_shuffle_flush(fs_plan* p) {
+  FS_REQUIRE(p, "bad arguments");
+  return (p->chunk > 1 && p->fill_chunk >= 0) ? launch_chunk(p) : FS_OK;
+}
+
 // Prepare round t's shuffles: device replay is enqueued here; a host replay job is queued
 // for the coordinator thread and this returns at once.
 extern "C" int fs_plan_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   FS_REQUIRE(p && (h_seeds || p->n.empty()) && t >= 0, "bad arguments");
   if (p->d.shuffle_device) {
+    if (p->chunk > 1) return chunk_shuffle(p, h_seeds, t);
     if (p->n.empty()) {
       p->slot_round[t & 1] = t;
       return FS_OK;
@@ -377,7 +484,29 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
   const fs_plan_desc& d = p->d;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int s = t & 1;
-  if (phases & FS_PHASE_TRAIN) {
+  if ((phases & FS_PHASE_TRAIN) && p->chunk > 1) {
+    const int K = p->chunk, c = t / K, r = t % K, sc = c & 1;
+    // a partly collected chunk (the last rounds of a run) is launched when first needed
+    if (p->slot_chunk[sc] != c && p->fill_chunk == c) {
+      const int rc = launch_chunk(p);
+      if (rc != FS_OK) return rc;
+    }
+    if (p->slot_chunk[sc] != c || r >= p->slot_nrounds[sc])
+      return fail(FS_EINVAL, "fs_plan_round: shuffles of this round were not prepared");
+    if (p->slot_waited[sc] != c) {                 // once per chunk
+      FS_HIP(hipStreamWaitEvent(st, p->uploaded[sc], 0), "fs_plan_round");
+      p->slot_waited[sc] = c;
+    }
+    const int rc = fs::local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[sc] + (int64_t)r * p->perm_len,
+                                  d.d_order, d.N, d.C, d.B, d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g,
+                                  d.d_W_out, d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, st,
+                                  p->max_client_steps);
+    if (rc != FS_OK) return rc;
+    if (r == p->slot_nrounds[sc] - 1) {            // the chunk's last round releases the slot
+      FS_HIP(hipEventRecord(p->consumed[sc], st), "fs_plan_round");
+      p->cons_recorded[sc] = true;
+    }
+  } else if (phases & FS_PHASE_TRAIN) {
     {
       // wait for this round's shuffle job (normally finished long ago)
       std::unique_lock<std::mutex> lk(p->m);
@@ -390,9 +519,10 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
       if (p->slot_round[s] != t) return fail(FS_EINVAL, "fs_plan_round: shuffles of this round were not prepared");
     }
     FS_HIP(hipStreamWaitEvent(st, p->uploaded[s], 0), "fs_plan_round");
-    const int rc = fs_local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[s], d.d_order, d.N, d.C, d.B,
-                                  d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g, d.d_W_out,
-                                  d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, stream);
+    const int rc = fs::local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[s], d.d_order, d.N, d.C, d.B,
+                                   d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g, d.d_W_out,
+                                   d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, st,
+                                   p->max_client_steps);
     if (rc != FS_OK) return rc;
     FS_HIP(hipEventRecord(p->consumed[s], st), "fs_plan_round");
     p->cons_recorded[s] = true;

@@ -242,6 +242,15 @@ class RoundPlan:
         _lib.check(_lib.lib().fs_plan_create(ctypes.byref(d), ctypes.byref(self._h)), 'fs_plan_create')
         self.npasses = int(trainer.N * trainer.E)
 
+    def set_chunk(self, rounds):
+        """Generate the shuffles of ``rounds`` consecutive rounds per launch (device replay;
+        before the first ``shuffle``): no cross-stream wait between the rounds of a chunk."""
+        _lib.check(_lib.lib().fs_plan_set_shuffle_chunk(self._h, int(rounds)), 'fs_plan_set_shuffle_chunk')
+
+    def flush(self):
+        """Launch a partly collected chunk of shuffles (after a run's last round was prepared)."""
+        _lib.check(_lib.lib().fs_plan_shuffle_flush(self._h), 'fs_plan_shuffle_flush')
+
     def shuffle(self, seeds, t):
         """seeds: [N*E] sampler seeds of round t's training passes (client-major)."""
         seeds = np.ascontiguousarray(seeds, dtype=np.int64)

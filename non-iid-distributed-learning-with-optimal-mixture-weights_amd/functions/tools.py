@@ -192,6 +192,17 @@ class Federation:
         # FedAMW: round t+1's shuffles (training and validation passes) are generated behind
         # round t's local training, beside its p-solve (one to 32 CUs busy), not beside the
         # training kernel, whose groups would wait for the CUs they hold
+        # FedAvg / FedProx with device-replayed shuffles: generate them K rounds per launch
+        # (FS_SHUFFLE_CHUNK, default 8; 1 = per round), one chunk ahead of the rounds that use
+        # them, so consecutive rounds run with no cross-stream wait between them.  FedAMW keeps
+        # per-round shuffles (its validation shuffles are double-buffered per round).
+        env_k = os.environ.get('FS_SHUFFLE_CHUNK')
+        self.chunk = 1
+        if self.mixture is None and shuffle_device:
+            self.chunk = max(1, min(int(env_k) if env_k else 8, R))
+            if self.chunk > 1:
+                self.plan.set_chunk(self.chunk)
+        self._prepared = 0              # next round whose shuffles are to be prepared
         self._train_done = None
         self.t = 0
         self.events = None              # a list: round() appends (phase, start, end) HIP timing events
@@ -208,6 +219,14 @@ class Federation:
                 self.side.wait_event(self._train_done)
             self.mixture.prepare(seeds[N * E:N * E + self.n_val_pass], t % 2, self.side)
 
+    def _prepare_upto(self, end):
+        """Prepare the shuffles of every round before ``min(end, R)`` not prepared yet, in order."""
+        while self._prepared < min(end, self.R):
+            self._prepare(self._prepared)
+            self._prepared += 1
+            if self._prepared == self.R and self.chunk > 1:
+                self.plan.flush()
+
     def round(self):
         """Run round t (tools.py:337-352 / 364-379 / 427-462) -- all launches async.  Round
         t+1's seeds are drawn (and its shuffles replayed) after round t is
@@ -215,7 +234,7 @@ class Federation:
         so this leaves the generator exactly where the reference leaves it after each call."""
         t = self.t
         if t == 0:
-            self._prepare(0)
+            self._prepare_upto(2 * self.chunk if self.chunk > 1 else 1)
         self.lr = update_learning_rate(t, self.lr, self.R)
         P = _lib.PHASE_TRAIN, _lib.PHASE_AGGREGATE, _lib.PHASE_EVAL
         ev = self.events
@@ -241,7 +260,7 @@ class Federation:
             # workgroups (FS_FEDAMW_SHUFFLE=late: after the round, beside the p-solve)
             early = self.t + 1 < self.R and os.environ.get('FS_FEDAMW_SHUFFLE', 'early') != 'late'
             if early:
-                self._prepare(t + 1)
+                self._prepare_upto(t + 2)
         if self.zshard:
             # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
@@ -271,8 +290,11 @@ class Federation:
         if self.W_hist is not None:
             self.W_hist[t].copy_(self.W_g)
         self.t += 1
-        if self.t < self.R and not early:
-            self._prepare(self.t)
+        if self.chunk > 1:
+            if t % self.chunk == 0 and t >= self.chunk:      # chunk c started: prepare chunk c + 1
+                self._prepare_upto(t + 2 * self.chunk)
+        elif self.t < self.R and not early:
+            self._prepare_upto(self.t + 1)
 
     def results(self):
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""

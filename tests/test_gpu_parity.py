@@ -83,6 +83,23 @@ def test_dropin_long_horizon_golden(amd, name):
         assert np.abs(stats['p'].cpu().numpy() - d['p'][-1]).max() <= P_RTOL * np.abs(d['p']).max()
 
 
+@pytest.mark.parametrize('chunk', ['1', '3', '7'])
+@pytest.mark.parametrize('name', [c for c in LONG_CASES if 'fedamw' not in c])
+def test_dropin_shuffle_chunks(amd, monkeypatch, name, chunk):
+    """Shuffles generated K rounds per launch (FS_SHUFFLE_CHUNK; the default is 8) give
+    bitwise the same run as one launch per round, including a partial last chunk (R = 20),
+    and leave the generator where the reference leaves it."""
+    d = load_long(name)
+    monkeypatch.setenv('FS_SHUFFLE_CHUNK', chunk)
+    (tr, tl, ta), st = run_dropin(amd, d)
+    after = torch.empty(4, dtype=torch.int64).random_()
+    monkeypatch.setenv('FS_SHUFFLE_CHUNK', '8')
+    (tr8, tl8, ta8), st8 = run_dropin(amd, d)
+    after8 = torch.empty(4, dtype=torch.int64).random_()
+    assert np.array_equal(st['W_rounds'], st8['W_rounds'])
+    assert torch.equal(tr, tr8) and torch.equal(tl, tl8) and torch.equal(ta, ta8) and torch.equal(after, after8)
+
+
 def test_dropin_consumes_rng_like_reference(amd):
     """After the call, the global generator must be where the reference left it."""
     d = load('fedprox_seq')
