@@ -287,6 +287,13 @@ int fs_plan_set_shuffle_chunk(fs_plan* plan, int rounds);
 /* ABI 7: launch a partly collected chunk now (after preparing a run's last round). */
 int fs_plan_shuffle_flush(fs_plan* plan);
 
+/* ABI 7, measurement: timing events recorded without a system-scope release (so timing a
+ * launch inside a round does not stall the next one); elapsed_ms synchronises on `end`. */
+int fs_timer_create(void** ev);
+int fs_timer_record(void* ev, void* stream);
+int fs_timer_elapsed_ms(void* start, void* end, float* ms);
+int fs_timer_destroy(void* ev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,10 @@ _SIGS = {
     'fs_plan_round': (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p]),
     'fs_plan_set_shuffle_chunk': (C.c_int, [C.c_void_p, C.c_int]),
     'fs_plan_shuffle_flush': (C.c_int, [C.c_void_p]),
+    'fs_timer_create': (C.c_int, [C.c_void_p]),
+    'fs_timer_record': (C.c_int, [C.c_void_p, C.c_void_p]),
+    'fs_timer_elapsed_ms': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    'fs_timer_destroy': (C.c_int, [C.c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -138,3 +142,25 @@ def source_revision():
         with open(f, 'rb') as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+class Timer:
+    """A timing event on the current stream without a system-scope release (fs_timer_*):
+    ``record()`` now, ``elapsed_time(other)`` in ms, as torch.cuda.Event's."""
+
+    def __init__(self):
+        self._ev = C.c_void_p()
+        check(lib().fs_timer_create(C.byref(self._ev)), 'fs_timer_create')
+
+    def record(self):
+        check(lib().fs_timer_record(self._ev, stream_ptr()), 'fs_timer_record')
+
+    def elapsed_time(self, end):
+        ms = C.c_float()
+        check(lib().fs_timer_elapsed_ms(self._ev, end._ev, C.byref(ms)), 'fs_timer_elapsed_ms')
+        return float(ms.value)
+
+    def __del__(self):
+        if getattr(self, '_ev', None) is not None and self._ev.value and _lib is not None:
+            _lib.fs_timer_destroy(self._ev)
+            self._ev = None

@@ -434,6 +434,35 @@ static int chunk_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   return r == K - 1 ? launch_chunk(p) : FS_OK;
 }
 
+// Timing events for measurement (bench.py's per-launch durations): timestamps, but no
+// system-scope release when recorded (hipEventDisableSystemFence) -- a default timing event
+// between two kernels of a round cost ~3.5 us of GPU idle each at config 2 (r02s2z).
+extern "C" int fs_timer_create(void** ev) {
+  FS_REQUIRE(ev, "null pointer");
+  hipEvent_t e = nullptr;
+  const char* f = getenv("FS_TIMER_FLAGS");        // diagnostics: raw hipEventCreateWithFlags flags
+  FS_HIP(hipEventCreateWithFlags(&e, f ? (unsigned)strtoul(f, nullptr, 0) : (unsigned)hipEventDisableSystemFence),
+         "fs_timer_create");
+  *ev = e;
+  return FS_OK;
+}
+extern "C" int fs_timer_record(void* ev, void* stream) {
+  FS_REQUIRE(ev, "null pointer");
+  FS_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(ev), reinterpret_cast<hipStream_t>(stream)), "fs_timer_record");
+  return FS_OK;
+}
+extern "C" int fs_timer_elapsed_ms(void* start, void* end, float* ms) {
+  FS_REQUIRE(start && end && ms, "null pointer");
+  FS_HIP(hipEventSynchronize(reinterpret_cast<hipEvent_t>(end)), "fs_timer_elapsed_ms");
+  FS_HIP(hipEventElapsedTime(ms, reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(end)),
+         "fs_timer_elapsed_ms");
+  return FS_OK;
+}
+extern "C" int fs_timer_destroy(void* ev) {
+  if (ev) FS_HIP(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)), "fs_timer_destroy");
+  return FS_OK;
+}
+
 extern "C" int fs_plan_shuffle_flush(fs_plan* p) {
   FS_REQUIRE(p, "bad arguments");
   return (p->chunk > 1 && p->fill_chunk >= 0) ? launch_chunk(p) : FS_OK;

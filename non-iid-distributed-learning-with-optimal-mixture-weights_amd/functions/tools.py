@@ -242,7 +242,7 @@ class Federation:
         def timed(name, fn):
             if ev is None:
                 return fn()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a, b = _lib.Timer(), _lib.Timer()     # no system-scope release (fs_timer_*)
             a.record()
             out = fn()
             b.record()
