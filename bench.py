@@ -136,7 +136,7 @@ def load_traffic(tag, kernel='local_train'):
         return None, 'no PMC capture for this workload'
     with open(path) as f:
         rec = json.load(f)
-    rev = _lib.source_revision()
+    rev = _lib.source_revision(kernel)
     if rec.get('source_rev') != rev:
         return None, 'stale PMC capture (kernel sources %s, measured on %s)' % (rev, rec.get('source_rev'))
     return rec, 'PMC %s' % rec.get('source', '')

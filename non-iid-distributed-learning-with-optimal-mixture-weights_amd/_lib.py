@@ -127,15 +127,26 @@ def stream_ptr(stream=None):
     return C.c_void_p(s.cuda_stream)
 
 
-def source_revision():
-    """sha256 (16 hex digits) of the device sources of libfedsim.so -- the kernels and the
-    headers they include (csrc/*.hip, csrc/*.h; host-only .cpp files and the C-ABI header
-    carry no device code).  Profiles under profiles/ record it; bench.py uses a PMC traffic
-    figure only when it was measured on kernels with this exact revision."""
+# the device sources each measured kernel is compiled from (its own file + the headers it includes)
+KERNEL_SOURCES = {
+    'local_train': ('local_train.hip', 'local_train_split.hip', 'common.h', 'lanes.h'),
+    'mix_solve': ('mixture.hip', 'common.h', 'lanes.h'),
+}
+
+
+def source_revision(kernel=None):
+    """sha256 (16 hex digits) of device sources of libfedsim.so: all of them (csrc/*.hip,
+    csrc/*.h; host-only .cpp files and the C-ABI header carry no device code), or only those
+    ``kernel`` ('local_train', 'mix_solve') is compiled from.  Profiles under profiles/
+    record it; bench.py uses a PMC traffic figure only when it was measured on the kernel's
+    exact sources."""
     import hashlib
     import glob
     pkg = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(pkg, 'csrc', '*.hip')) + glob.glob(os.path.join(pkg, 'csrc', '*.h')))
+    if kernel:
+        files = sorted(os.path.join(pkg, 'csrc', f) for f in KERNEL_SOURCES[kernel])
+    else:
+        files = sorted(glob.glob(os.path.join(pkg, 'csrc', '*.hip')) + glob.glob(os.path.join(pkg, 'csrc', '*.h')))
     h = hashlib.sha256()
     for f in files:
         h.update(os.path.basename(f).encode())

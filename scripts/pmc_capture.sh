@@ -7,8 +7,8 @@ export TMPDIR=/tmp
 TAG=$1; ARGS=$2; REGEX=$3
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
-python3 -c "import sys; sys.path.insert(0, '.'); import fedamw_amd; from fedamw_amd import _lib; print(_lib.source_revision())" \
-  > $OUT/source_rev.txt || exit 1
+python3 -c "import sys, json; sys.path.insert(0, '.'); import fedamw_amd; from fedamw_amd import _lib; print(json.dumps({k: _lib.source_revision(k) for k in [None] + list(_lib.KERNEL_SOURCES)}))" \
+  > $OUT/source_rev.json || exit 1
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS" \

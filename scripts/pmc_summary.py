@@ -30,10 +30,16 @@ def main():
             k = r['Kernel_Name'].split('(')[0].replace('void ', '')
             vals[(k, r['Counter_Name'])].append(float(r['Counter_Value']))
     # the kernel-source revision the passes ran on (written by pmc_capture.sh on the GPU box)
-    rev_file = os.path.join(src, 'source_rev.txt')
-    rev = open(rev_file).read().strip() if os.path.exists(rev_file) else (sys.argv[4] if len(sys.argv) > 4 else None)
+    # (source_rev.json: the revision of all device sources ("null") and of each measured kernel's)
+    revs = {}
+    if os.path.exists(os.path.join(src, 'source_rev.json')):
+        revs = json.load(open(os.path.join(src, 'source_rev.json')))
+    elif os.path.exists(os.path.join(src, 'source_rev.txt')):
+        revs = {'null': open(os.path.join(src, 'source_rev.txt')).read().strip()}
+    kkey = kname.replace('_kernel', '')
+    rev = revs.get(kkey) or revs.get('null') or (sys.argv[4] if len(sys.argv) > 4 else None)
     if not rev:
-        raise SystemExit('no source_rev.txt in %s: pass the revision the capture ran on as argv[4]' % src)
+        raise SystemExit('no source_rev.json in %s: pass the revision the capture ran on as argv[4]' % src)
     lines = ['# PMC summary %s (kernel sources %s); per-dispatch means' % (tag, rev)]
     for (k, c), v in sorted(vals.items()):
         lines.append('%-60s %-26s n=%-3d mean=%.6g' % (k[:60], c, len(v), sum(v) / len(v)))
