@@ -1187,6 +1187,12 @@ static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, con
 // ----------------------------------------------------------------------------
 constexpr int MQ_WAVES = 4;
 
+typedef float float2v __attribute__((ext_vector_type(2)));
+// elements (2h, 2h+1) of a float4
+__device__ __forceinline__ float2v half2(const floatx4& v, int h) {
+  return h ? float2v{v[2], v[3]} : float2v{v[0], v[1]};
+}
+
 template <int NK, int CL, int DEPTH, int SPL>
 __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
@@ -1291,7 +1297,11 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     _Pragma("unroll") for (int c = 0; c < 16; ++c) {                                         \
       float a = 0.f;                                                                         \
       if (c < CL) {                                                                          \
-        _Pragma("unroll") for (int j = 0; j < NK; ++j) a += zr[R_][c][j >> 2][j & 3] * pr[j]; \
+        /* packed pairs (v_pk_fma_f32): even and odd clients summed apart, then joined */    \
+        float2v a2 = {0.f, 0.f};                                                             \
+        _Pragma("unroll") for (int j = 0; j < NK; j += 2) a2 = __builtin_elementwise_fma(   \
+            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2);          \
+        a = a2.x + a2.y;                                                                     \
       }                                                                                      \
       v[c] = a;                                                                              \
     }                                                                                        \
@@ -1314,10 +1324,16 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     gb[w][lane] = g;                                                                         \
     float gv[CL];                                                                            \
     _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
-    float gme[NK];                                                                           \
-    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                             \
+    float2v gm2[NK / 2];                                                                      \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = float2v{0.f, 0.f};            \
     _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
-      _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] += gv[c] * zr[R_][c][j >> 2][j & 3]; \
+      _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = __builtin_elementwise_fma( \
+          float2v{gv[c], gv[c]}, half2(zr[R_][c][j >> 1], j & 1), gm2[j]);                   \
+    }                                                                                        \
+    float gme[NK];                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) {                                     \
+      gme[2 * j] = gm2[j].x;                                                                 \
+      gme[2 * j + 1] = gm2[j].y;                                                             \
     }                                                                                        \
     MR_STAMP(2)                                                                              \
     /* slot consumed: refill with step s + DEPTH, then fetch the rows of s + 2 DEPTH */      \
