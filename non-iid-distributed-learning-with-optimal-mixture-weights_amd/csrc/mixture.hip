@@ -1193,7 +1193,7 @@ __device__ __forceinline__ float2v half2(const floatx4& v, int h) {
   return h ? float2v{v[2], v[3]} : float2v{v[0], v[1]};
 }
 
-template <int NK, int CL, int DEPTH, int SPL>
+template <int NK, int CL, int DEPTH, int SPL, bool FASTX>
 __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
     int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
@@ -1316,11 +1316,16 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     const float o = rs_pair(v[0], v[1], 1, lane);  /* class r's logit */                     \
     const bool real = r < C;                                                                 \
     const float m = row16_all<true>(real ? o : -INFINITY);                                   \
-    const float ssum = row16_all<false>(real ? expf(o - m) : 0.f);                           \
     const float invb = bc == Bv ? invB : invT;                                               \
-    const float g = (real && brow < bc)                                                      \
-                        ? (r == labq[R_] ? -invb : 0.f) + expf(o - m - logf(ssum)) * invb    \
-                        : 0.f;                                                               \
+    float g;                                                                                 \
+    if constexpr (FASTX) {         /* v_exp_f32 / v_rcp_f32: softmax = e / sum */            \
+      const float e = real ? __expf(o - m) : 0.f;                                            \
+      const float ssum = row16_all<false>(e);                                                \
+      g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + e * __builtin_amdgcn_rcpf(ssum) * invb : 0.f; \
+    } else {                       /* torch's log_softmax backward: exp(o - m - log(sum)) */ \
+      const float ssum = row16_all<false>(real ? expf(o - m) : 0.f);                         \
+      g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + expf(o - m - logf(ssum)) * invb : 0.f; \
+    }                                                                                        \
     gb[w][lane] = g;                                                                         \
     float gv[CL];                                                                            \
     _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
@@ -1407,9 +1412,18 @@ static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, co
   // ring: DEPTH x CL x NK floats per lane (<= 160), CL*NK/4 + 2 loads per step in the vmcnt window
   constexpr int depth = (3 * CL * NK <= 160 && 3 * (CL * NK / 4 + 2) <= 63) ? 3 : 2;
   const int blocks = pf.prog ? 8 * std::min(pf.h, 31) + 1 : 1;   // helpers: the solver's XCD only
-  hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z, y,
-                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31), pf.lead,
-                     quad_oob());
+  // softmax on v_exp_f32 / v_rcp_f32 (e / sum) by default: config 2 1.28-1.29 -> 1.21-1.23 us per
+  // step (r02s2fx), within the fp32 tolerance of the oracle like every other solver;
+  // FS_MIX_QUAD_FASTEXP=0: torch's exp(o - m - log(sum)) form with libm expf / logf
+  const char* fx = getenv("FS_MIX_QUAD_FASTEXP");
+  if (!(fx && atoi(fx) == 0))
+    hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL, true>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z,
+                       y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
+                       pf.lead, quad_oob());
+  else
+    hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL, false>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z,
+                       y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
+                       pf.lead, quad_oob());
 }
 
 static bool quad_covers(int N, int C, int Bv, int nv, int epochs) {

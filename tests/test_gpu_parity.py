@@ -446,6 +446,16 @@ def test_mix_solve_quad(amd, monkeypatch, N, C, nv, Bv):
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
 
 
+@pytest.mark.parametrize('N,C,nv,Bv', [(100, 10, 517, 16), (60, 8, 33, 9), (37, 16, 90, 16)])
+def test_mix_solve_quad_libm_softmax(amd, monkeypatch, N, C, nv, Bv):
+    """The quarter-wave solver with torch's softmax form on libm expf / logf
+    (FS_MIX_QUAD_FASTEXP=0; the default is v_exp / v_rcp) vs the oracle."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
+    monkeypatch.setenv('FS_MIX_QUAD_FASTEXP', '0')
+    test_mix_solve_variants(amd, N, C, nv, Bv)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
+
+
 @pytest.mark.parametrize('split', [5, 7, 10])
 @pytest.mark.parametrize('oob', [0, 1])
 def test_mix_solve_quad_issue_forms(amd, monkeypatch, split, oob):
