@@ -41,6 +41,11 @@ def test_abi_version():
     (lambda L: L.fs_eval(None, 64, None, 0, None, 10, None, None, None), 'n'),
     (lambda L: L.fs_mix_solve(None, None, None, 5, 3, 10, 1, 65, 0.1, 0.9, None, None, None, None, 0, None),
      'batch'),
+    (lambda L: L.fs_plan_set_shuffle_chunk(None, 8), 'bad arguments'),
+    (lambda L: L.fs_plan_shuffle_flush(None), 'bad arguments'),
+    (lambda L: L.fs_timer_create(None), 'null'),
+    (lambda L: L.fs_timer_record(None, None), 'null'),
+    (lambda L: L.fs_timer_elapsed_ms(None, None, None), 'null'),
 ])
 def test_invalid_arguments_fail_without_touching_the_gpu(call, needle):
     L = _lib.lib()
