@@ -62,7 +62,7 @@ ABI_VERSION = 7
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
-SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows', 8: 'quad'}
+SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows', 8: 'quad', 9: 'qmc'}
 
 
 class PlanDesc(C.Structure):

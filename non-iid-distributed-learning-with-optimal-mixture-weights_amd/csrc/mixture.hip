@@ -1904,6 +1904,264 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   return 0;
 }
 
+// ----------------------------------------------------------------------------
+// p-solve, multi-CU quarter-wave form "qmc" (Bv <= 16, 128 < N <= 16 * 16 * NK, C <= CL):
+// the quarter-wave layout on K <= 16 workgroups of 16*NK clients each (N = 1000: K = 8),
+// all on one XCD.  A workgroup computes its clients' partial logits, publishes them (the
+// 16 x C row/class values, 8-byte {tag, value} granules) and reads the K partials of every
+// value back -- ONE hop -- summing them in workgroup order, so every workgroup holds the
+// bitwise-same logits, softmax and CE gradient; the gradient of its own clients, the
+// momentum step and p stay local (no second hop).  Its 16 x C x 16NK Z values per step come
+// from L2, where H helper workgroups on the same XCD prefetch the rows of the next steps
+// (FS_MIX_PF_H, default 16 for this solver).  Spins are bounded; a timeout sets the error
+// word and poisons p with NaN.
+// ----------------------------------------------------------------------------
+constexpr int QMC_KMAX = 16;
+
+template <int NK, int CL, int DEPTH, int SPL>
+__global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
+    const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
+    int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
+    int* __restrict__ first_flag, int z_bytes, unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err,
+    int K, unsigned spin_limit, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead) {
+  static_assert(NK == 4 || NK == 8, "clients per lane");
+  static_assert(CL >= 1 && CL <= 16, "classes");
+  static_assert(DEPTH * (CL * NK / 4 + 2) <= 63, "ring vs the vmcnt window");
+  if (blockIdx.x % MC_XCDS) return;
+  const int bk = blockIdx.x / MC_XCDS;
+  if (bk >= K) {                                   // L2 prefetch helpers on the solvers' XCD
+    if (pf_prog && bk - K < pf_h) mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, bk - K, pf_h, pf_lead, pf_prog);
+    return;
+  }
+  const int k = bk;
+  constexpr int NV4 = NK / 4;
+  constexpr int KP = NK / 4;
+  __shared__ __attribute__((aligned(16))) float gx[2][MQ_WAVES][64 * KP];
+  __shared__ __attribute__((aligned(16))) float gb[MQ_WAVES][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r = lane & 15;
+  const int brow = MQ_WAVES * w + q;
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int bc_tail = nv - (nbat - 1) * Bv;
+  const float invB = 1.0f / (float)Bv;
+  const float invT = 1.0f / (float)bc_tail;
+  const int n0 = k * 16 * NK + NK * r;             // this lane's first client (global index)
+  float pr[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) pr[j] = n0 + j < N ? p[n0 + j] : 0.f;
+  const int kj0 = (q >> 1) * (NK / 2) + (q & 1) * (NK / 4);
+  float po[KP], bo[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int n = n0 + kj0 + i;
+    po[i] = n < N ? p[n] : 0.f;
+    bo[i] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  uint32_t lofs[NV4];                              // chunks past ldN: out of range (zeros, no access)
+#pragma unroll
+  for (int h = 0; h < NV4; ++h) lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : 0x80000000u;
+  int sofs[CL];
+#pragma unroll
+  for (int c = 0; c < CL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * ldN);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
+  int fst = 0, fep = 0, fsb = 0;
+  auto fetch_row = [&]() -> int {
+    const int base = fep * nv + fsb * Bv;
+    const int bcf = min(Bv, nv - fsb * Bv);
+    const int row = perms[base + (brow < bcf ? brow : 0)];
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+    return row;
+  };
+  floatx4 zr[DEPTH][CL][NV4];
+  int idxq[DEPTH], labq[DEPTH];
+#define QM_ISSUE(R_, ROW_, C0_, C1_)                                                         \
+  {                                                                                          \
+    const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
+    _Pragma("unroll") for (int c = C0_; c < C1_; ++c) {                                      \
+      _Pragma("unroll") for (int h = 0; h < NV4; ++h) zr[R_][c][h] = __builtin_bit_cast(     \
+          floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[h], sofs[c], 0));   \
+    }                                                                                        \
+  }
+#pragma unroll
+  for (int kk = 0; kk < DEPTH; ++kk) {
+    const int row = fetch_row();
+    labq[kk] = y[row];
+    QM_ISSUE(kk, row, 0, CL);
+  }
+#pragma unroll
+  for (int kk = 0; kk < DEPTH; ++kk) idxq[kk] = fetch_row();
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  bool dead = false;
+  if (spin_limit == 0 && k == 0 && tid == 0 && total > 0)   // test knob: report an injected timeout
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int csb = 0;
+  int s = 0;
+  int late_row = 0;
+#define QM_STEP(R_)                                                                          \
+  {                                                                                          \
+    if (s >= total) break;                                                                   \
+    const int bc = min(Bv, nv - csb * Bv);                                                   \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
+    float v[16];                                                                             \
+    _Pragma("unroll") for (int c = 0; c < 16; ++c) {                                         \
+      float a = 0.f;                                                                         \
+      if (c < CL) {                                                                          \
+        float2v a2 = {0.f, 0.f};                                                             \
+        _Pragma("unroll") for (int j = 0; j < NK; j += 2) a2 = __builtin_elementwise_fma(   \
+            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2);          \
+        a = a2.x + a2.y;                                                                     \
+      }                                                                                      \
+      v[c] = a;                                                                              \
+    }                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) v[i] = rs_bank<8>(v[i], v[i + 8]);         \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) v[i] = rs_bank<4>(v[i], v[i + 4]);         \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
+    const float opart = rs_pair(v[0], v[1], 1, lane);   /* this workgroup's share */         \
+    const bool real = r < C;                                                                 \
+    /* one hop: publish, read the K partials, fold in workgroup order */                     \
+    const unsigned tag = (unsigned)s + 1u;                                                   \
+    unsigned long long* slot = xbuf + (int64_t)(s & 1) * K * MC_SLOT;                        \
+    const int gi = brow * 16 + r;                                                            \
+    float o = 0.f;                                                                           \
+    if (real) {                                                                              \
+      __hip_atomic_store(slot + (int64_t)k * MC_SLOT + gi,                                   \
+                         ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(opart), \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                        \
+      unsigned long long gr[QMC_KMAX];                                                       \
+      _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
+        if (kk < K) gr[kk] = __hip_atomic_load(slot + (int64_t)kk * MC_SLOT + gi, __ATOMIC_RELAXED, \
+                                               __HIP_MEMORY_SCOPE_AGENT);                    \
+      _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk) {                              \
+        if (kk < K && !dead && (unsigned)(gr[kk] >> 32) != tag) {                            \
+          unsigned long long g_ = 0;                                                         \
+          if (mc_wait(slot + (int64_t)kk * MC_SLOT + gi, tag, g_, spin_limit, err)) gr[kk] = g_; \
+          else dead = true;                                                                  \
+        }                                                                                    \
+      }                                                                                      \
+      _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
+        if (kk < K) o += __uint_as_float((unsigned)gr[kk]);                                  \
+    }                                                                                        \
+    /* the late classes of step s - 1 + DEPTH, behind the hop (its polls queue behind nothing) */ \
+    if constexpr (SPL < CL) {                                                                \
+      if (s > 0) QM_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
+    }                                                                                        \
+    const float m = row16_all<true>(real ? o : -INFINITY);                                   \
+    const float invb = bc == Bv ? invB : invT;                                               \
+    const float e = real ? __expf(o - m) : 0.f;                                              \
+    const float ssum = row16_all<false>(e);                                                  \
+    const float g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + e * __builtin_amdgcn_rcpf(ssum) * invb \
+                                        : 0.f;                                               \
+    gb[w][lane] = g;                                                                         \
+    float gv[CL];                                                                            \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
+    float2v gm2[NK / 2];                                                                     \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = float2v{0.f, 0.f};           \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
+      _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = __builtin_elementwise_fma( \
+          float2v{gv[c], gv[c]}, half2(zr[R_][c][j >> 1], j & 1), gm2[j]);                   \
+    }                                                                                        \
+    float gme[NK];                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) {                                     \
+      gme[2 * j] = gm2[j].x;                                                                 \
+      gme[2 * j + 1] = gm2[j].y;                                                             \
+    }                                                                                        \
+    labq[R_] = y[idxq[R_]];                                                                  \
+    QM_ISSUE(R_, idxq[R_], 0, SPL);                                                          \
+    late_row = idxq[R_];                                                                     \
+    idxq[R_] = fetch_row();                                                                  \
+    float t[NK / 2];                                                                         \
+    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = rs_level<32, true>(gme[i], gme[i + NK / 2], lane); \
+    float u[KP];                                                                             \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = rs_level<16, true>(t[i], t[i + KP], lane); \
+    const int par = s & 1;                                                                   \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
+    lds_barrier();                                                                           \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
+      float gs = gx[par][0][lane * KP + i];                                                  \
+      _Pragma("unroll") for (int kk = 1; kk < MQ_WAVES; ++kk) gs += gx[par][kk][lane * KP + i]; \
+      if (n0 + kj0 + i < N) momentum_step(po[i], bo[i], gs, first, mom, lr);                 \
+    }                                                                                        \
+    first = 0;                                                                               \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \
+    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
+    ++s;                                                                                     \
+    if (pf_prog && k == 0 && (s & 3) == 0) mix_publish_progress(pf_prog, s);                 \
+  }
+  for (;;) {
+    QM_STEP(0)
+    if constexpr (DEPTH > 1) QM_STEP(1)
+    if constexpr (DEPTH > 2) QM_STEP(2)
+  }
+#undef QM_STEP
+#undef QM_ISSUE
+  if (pf_prog && k == 0) mix_publish_progress(pf_prog, total);
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int n = n0 + kj0 + i;
+      if (n < N) {
+        p[n] = dead ? __int_as_float(0x7fc00000) : po[i];
+        buf[n] = bo[i];
+      }
+    }
+    if (k == 0 && lane == 0 && total > 0) *first_flag = 0;
+  }
+}
+
+// clients per lane: 8 (128 per workgroup) for C <= 10, else 4; FS_MIX_QMC_NK=4 forces 4 (diagnostics)
+static int qmc_nk(int C) {
+  const char* e = getenv("FS_MIX_QMC_NK");
+  return (C <= 10 && !(e && atoi(e) == 4)) ? 8 : 4;
+}
+
+static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
+  const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
+  const int nk = qmc_nk(C);
+  return Bv <= 16 && N > 128 && C <= 16 && (mix_ldn(N) + 16 * nk - 1) / (16 * nk) <= QMC_KMAX &&
+         zb < ((int64_t)1 << 31) && (int64_t)epochs * nv < ((int64_t)1 << 31);
+}
+
+// 1: not covered; 0: launched; < 0: error
+static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
+                         int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first, void* d_ws,
+                         int64_t ws_bytes, MixPrefetch pf) {
+  if (!qmc_covers(N, C, Bv, nv, epochs)) return 1;
+  const int nk = qmc_nk(C);
+  const int K = (mix_ldn(N) + 16 * nk - 1) / (16 * nk);
+  const int64_t xbytes = mc_xbytes(K);
+  if (!d_ws || ws_bytes < xbytes + MC_ERR_BYTES)
+    return fail(FS_EINVAL, "fs_mix_solve: workspace too small (see fs_mix_solve_ws_bytes)");
+  unsigned long long* ws = reinterpret_cast<unsigned long long*>(d_ws);
+  unsigned* err = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES);
+  hipError_t e = hipMemsetAsync(ws, 0, (size_t)xbytes, st);
+  if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
+  const unsigned spin_limit = mc_spin_limit();
+  const int h = pf.prog ? std::min(pf.h, 32 - K) : 0;   // the solvers' XCD has 32 CUs
+  const dim3 grid(MC_XCDS * (K + h)), block(MQ_WAVES * 64);
+  const int zb = (int)((int64_t)nv * C * mix_ldn(N) * 4);
+  if (nk == 8)
+    hipLaunchKernelGGL((mix_solve_qmc_kernel<8, 10, 2, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+  else if (C <= 10)
+    hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 10, 3, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+  else
+    hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 16, 2, quad_split<16>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+  return 0;
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -1955,7 +2213,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
     const char* eh = getenv("FS_MIX_PF_H");
     const char* el = getenv("FS_MIX_PF_LEAD");
-    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : 0);
+    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : (want == "qmc" ? 16 : 0));
     const int lead = el ? std::max(1, atoi(el)) : 16;
     if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
       pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
@@ -2003,6 +2261,16 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     if (rc < 0) return rc;
     if (rc == 1) {
       t_last_solver = 7;
+      FS_LAUNCH_CHECK();
+      return FS_OK;
+    }
+  }
+  if (want == "qmc") {
+    const int rc = mix_solve_qmc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
+                                 d_first, d_ws, ws_bytes, pf);
+    if (rc < 0) return rc;
+    if (rc == 0) {
+      t_last_solver = 9;
       FS_LAUNCH_CHECK();
       return FS_OK;
     }

@@ -408,6 +408,32 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S, hops):
     assert mode == 2, mode             # the multi-CU solver ran (a timed-out spin raises in check_errors)
 
 
+@pytest.mark.parametrize('h', ['0', '16'])
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (1000, 10, 97, 16),     # config 5 client count: K = 8 workgroups of 128 clients
+    (300, 4, 60, 16),       # K = 3, ragged last slice
+    (129, 3, 77, 8),        # K = 2, Bv < 16, ragged last batch
+    (2000, 2, 45, 16),      # K = 16
+    (1000, 16, 40, 16),     # C = 16: 64 clients per workgroup, K = 16
+    (200, 10, 133, 16),     # K = 2
+])
+def test_mix_solve_qmc(amd, monkeypatch, N, C, nv, Bv, h):
+    """fs_mix_solve's multi-CU quarter-wave solver (clients over K workgroups, one exchange of
+    the partial logits per step; with / without L2 prefetch helpers) vs the oracle's p-SGD."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'qmc')
+    monkeypatch.setenv('FS_MIX_PF_H', h)
+    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
+
+
+def test_mix_solve_qmc_timeout_raises(amd, monkeypatch):
+    """A timed-out exchange of the multi-CU quarter-wave solver sets the error word."""
+    monkeypatch.setenv('FS_MIX_SOLVER', 'qmc')
+    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
+    with pytest.raises(amd.lib.FedsimError):
+        test_mix_solve_variants(amd, 300, 4, 60, 16)
+
+
 @pytest.mark.parametrize('rw', [1, 2, 4, 8])
 @pytest.mark.parametrize('N,C,nv,Bv', [
     (100, 10, 517, 16),     # config 2 shape: NK = 2, CP = 16
