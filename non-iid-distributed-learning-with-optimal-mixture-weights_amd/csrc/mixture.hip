@@ -2205,6 +2205,8 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   const std::string want = pick ? pick : "auto";
   const bool use_quad = (want == "auto" && !(N <= 16 && C <= 4) && quad_covers(N, C, Bv, n_val, epochs)) ||
                         want == "quad";
+  // the multi-CU quarter-wave solver where the single-workgroup register solvers end (N > 256)
+  const bool use_qmc = want == "qmc" || (want == "auto" && N > 256 && qmc_covers(N, C, Bv, n_val, epochs));
   MixPrefetch pf{nullptr, 0, 0};
   {
     // L2 prefetch helpers of the single-CU solvers: FS_MIX_PF_H helper workgroups (0 = off;
@@ -2213,7 +2215,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
     const char* eh = getenv("FS_MIX_PF_H");
     const char* el = getenv("FS_MIX_PF_LEAD");
-    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : (want == "qmc" ? 16 : 0));
+    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : (use_qmc ? 16 : 0));
     const int lead = el ? std::max(1, atoi(el)) : 16;
     if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
       pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
@@ -2225,8 +2227,10 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   }
   // auto: one wave for N <= 16, C <= 4; the quarter-wave solver (+ L2 prefetch helpers) for
   // N <= 64, C <= 16 or N <= 128, C <= 10; the register solvers where an instance covers the
-  // shape (no cross-CU exchange: ~1-2.5 us per step); else the multi-CU solver (~4-7 us per
-  // step, 7-11x the single-workgroup staged / global solvers at N = 200..1000, C = 10); else those.
+  // shape (no cross-CU exchange: ~1-2.5 us per step); for N > 256 the multi-CU quarter-wave
+  // solver (one exchange hop per step; 3.9 us at N = 1000, C = 10) where it covers, else the
+  // multi-CU solver (two hops, ~4-7 us per step, 7-11x the single-workgroup staged / global
+  // solvers at N = 200..1000, C = 10); else those.
   if (((want == "auto" && N <= 16 && C <= 4 && Bv <= 16) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
     hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
                        Bv, lr_p, momentum, d_p, d_buf, d_first);
@@ -2265,7 +2269,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
       return FS_OK;
     }
   }
-  if (want == "qmc") {
+  if (use_qmc) {
     const int rc = mix_solve_qmc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
                                  d_first, d_ws, ws_bytes, pf);
     if (rc < 0) return rc;

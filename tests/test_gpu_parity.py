@@ -363,7 +363,8 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
 @pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'wave'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
                                            (10, 5, 16, 'quad'), (100, 10, 16, 'quad'), (64, 16, 16, 'quad'),
                                            (37, 20, 16, 'reg'), (129, 3, 16, 'reg2'), (200, 4, 16, 'reg2'),
-                                           (1000, 10, 16, 'mc'), (23, 5, 24, 'staged')])
+                                           (1000, 10, 16, 'qmc'), (300, 4, 16, 'qmc'), (1100, 16, 16, 'mc'),
+                                           (23, 5, 24, 'staged')])
 def test_mix_solve_auto_choice(amd, N, C, Bv, solver):
     """The solver fs_mix_solve picks by shape."""
     rs = np.random.RandomState(N)
