@@ -682,7 +682,7 @@ def test_fedamw_dropin_many_clients_vs_oracle(amd, N):
     tr, tl, ta = amd.tools.FedAMW([T(x) for x in Xs], [T(y) for y in ys], T(Xt), T(yt), _dl(Xv, yv),
                                   'classification', C, D, 0.5, 2, 32, False, 0.0, True, 1e-3, R, lr_p,
                                   clients='parallel', stats=stats, verbose=False)
-    assert amd.lib.lib().fs_mix_solve_last_mode() == 2     # the multi-CU solver ran (results() checks its error word)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] in ('mc', 'qmc')   # a multi-CU solver ran (results() checks its error word)
     torch.manual_seed(5)
     otr, otl, ota, trace = O.FedAMW(Xs, ys, Xt, yt, Xv, yv, 'classification', C, D, 0.5, 2, 32, False, 0.0, True,
                                     1e-3, R, lr_p, clients='parallel')
