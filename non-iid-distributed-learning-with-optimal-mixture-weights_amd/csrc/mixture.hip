@@ -2216,6 +2216,10 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     const char* eh = getenv("FS_MIX_PF_H");
     const char* el = getenv("FS_MIX_PF_LEAD");
     const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : (use_qmc ? 16 : 0));
+    // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
+    // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
+    // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
+    // 16 is still the fastest: 3.85 us per step vs 4.75 at leads 2-4 (r02s2lead)
     const int lead = el ? std::max(1, atoi(el)) : 16;
     if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
       pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
