@@ -2203,8 +2203,10 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // and tests; a forced solver that does not cover the shape falls through to the next one)
   const char* pick = getenv("FS_MIX_SOLVER");
   const std::string want = pick ? pick : "auto";
-  const bool use_quad = (want == "auto" && !(N <= 16 && C <= 4) && quad_covers(N, C, Bv, n_val, epochs)) ||
-                        want == "quad";
+  // one wave where it measured fastest (N <= 16, C = 3..4: 0.616 vs 0.62 us per step); the
+  // quarter-wave solver from C <= 2 (config 1, N = 10: 0.574 vs 0.617 us, r02s2c1b) upwards
+  const bool auto_wave = N <= 16 && C >= 3 && C <= 4 && Bv <= 16;
+  const bool use_quad = (want == "auto" && !auto_wave && quad_covers(N, C, Bv, n_val, epochs)) || want == "quad";
   // the multi-CU quarter-wave solver where the single-workgroup register solvers end (N > 256)
   const bool use_qmc = want == "qmc" || (want == "auto" && N > 256 && qmc_covers(N, C, Bv, n_val, epochs));
   MixPrefetch pf{nullptr, 0, 0};
@@ -2215,7 +2217,9 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
     const char* eh = getenv("FS_MIX_PF_H");
     const char* el = getenv("FS_MIX_PF_LEAD");
-    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : (use_quad ? 4 : (use_qmc ? 16 : 0));
+    // (quad: only when Z outgrows the L2s -- at config 1's 0.6 MB the helpers cost 3 %, r02s2c1)
+    const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
+    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0));
     // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
     // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
     // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
@@ -2235,7 +2239,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // solver (one exchange hop per step; 3.9 us at N = 1000, C = 10) where it covers, else the
   // multi-CU solver (two hops, ~4-7 us per step, 7-11x the single-workgroup staged / global
   // solvers at N = 200..1000, C = 10); else those.
-  if (((want == "auto" && N <= 16 && C <= 4 && Bv <= 16) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
+  if (((want == "auto" && auto_wave) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
     hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
                        Bv, lr_p, momentum, d_p, d_buf, d_first);
     t_last_solver = 6;

@@ -318,7 +318,7 @@ def test_eval_unit_golden(amd):
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [
-    (10, 2, 203, 16),       # config 1 shape: one-wave solver
+    (10, 2, 203, 16),       # config 1 shape: quarter-wave solver (C <= 2)
     (16, 4, 77, 16),        # one wave, every lane's class real, ragged last batch
     (5, 3, 40, 7),          # one wave, Bv < 16 (idle rows), N not a multiple of 4
     (1, 2, 33, 16),         # one client
@@ -360,7 +360,7 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
-@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'wave'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
+@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'quad'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
                                            (10, 5, 16, 'quad'), (100, 10, 16, 'quad'), (64, 16, 16, 'quad'),
                                            (37, 20, 16, 'reg'), (129, 3, 16, 'reg2'), (200, 4, 16, 'reg2'),
                                            (1000, 10, 16, 'qmc'), (300, 4, 16, 'qmc'), (1100, 16, 16, 'mc'),
@@ -546,7 +546,8 @@ def test_mix_solve_rows_timeout_raises(amd, monkeypatch):
 
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
-                                        ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('reg2-select', 100, 10),
+                                        ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('wave', 10, 2),
+                                        ('reg2-select', 100, 10),
                                         ('reg2-select', 129, 3)])
 def test_mix_solve_forced_fallbacks(amd, monkeypatch, solver, N, C):
     """The solvers the auto choice does not take at these shapes (reg2-select: form 2 with the
