@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 7
+#define FS_ABI_VERSION 8
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -220,6 +220,13 @@ int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, i
  *                       round t; losses to d_loss_hist[t*N .. t*N+N)
  *   FS_PHASE_AGGREGATE  fs_aggregate(W_out, p) -> d_W_g  (p = d_p, or the override)
  *   FS_PHASE_EVAL       fs_eval(d_W_g) -> d_eval_hist[2t], [2t+1]
+ *   FS_PHASE_EVAL_DEFER (with FS_PHASE_EVAL) round t's evaluation may ride on the
+ *                       next call's TRAIN launch, on the CUs its client groups
+ *                       leave idle (parallel split launches, C <= 16; the same
+ *                       per-row arithmetic as fs_eval).  d_eval_hist[2t..] is then
+ *                       written by that call; a call without TRAIN, or an AGGREGATE,
+ *                       runs the pending evaluation on its own first.  Do not
+ *                       defer the last round's evaluation.
  * fs_plan_shuffle(plan, seeds, t) replays round t's N*E training shuffles
  * (DataLoader passes of tools.py:179, client-major / epoch-minor seeds) into slot
  * t % 2 on the plan's side stream -- on the GPU (fs_randperm_device, default) or on
@@ -231,6 +238,7 @@ int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, i
 #define FS_PHASE_TRAIN 1
 #define FS_PHASE_AGGREGATE 2
 #define FS_PHASE_EVAL 4
+#define FS_PHASE_EVAL_DEFER 8
 
 typedef struct fs_plan fs_plan;
 
@@ -286,6 +294,9 @@ int fs_plan_round(fs_plan* plan, int t, float lr, int phases, const float* d_p_o
 int fs_plan_set_shuffle_chunk(fs_plan* plan, int rounds);
 /* ABI 7: launch a partly collected chunk now (after preparing a run's last round). */
 int fs_plan_shuffle_flush(fs_plan* plan);
+/* ABI 8: evaluation workgroups a TRAIN launch of this plan carries for FS_PHASE_EVAL_DEFER
+ * (0: the plan evaluates with launches of its own; FS_EVAL_FUSE=0 at creation forces 0). */
+int fs_plan_eval_blocks(const fs_plan* plan);
 
 /* ABI 7, measurement: timing events recorded without a system-scope release (so timing a
  * launch inside a round does not stall the next one); elapsed_ms synchronises on `end`. */

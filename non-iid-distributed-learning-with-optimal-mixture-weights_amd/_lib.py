@@ -51,6 +51,7 @@ _SIGS = {
     'fs_plan_round': (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p]),
     'fs_plan_set_shuffle_chunk': (C.c_int, [C.c_void_p, C.c_int]),
     'fs_plan_shuffle_flush': (C.c_int, [C.c_void_p]),
+    'fs_plan_eval_blocks': (C.c_int, [C.c_void_p]),
     'fs_timer_create': (C.c_int, [C.c_void_p]),
     'fs_timer_record': (C.c_int, [C.c_void_p, C.c_void_p]),
     'fs_timer_elapsed_ms': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -58,9 +59,9 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
-PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL = 1, 2, 4
+PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
 SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows', 8: 'quad', 9: 'qmc'}
 

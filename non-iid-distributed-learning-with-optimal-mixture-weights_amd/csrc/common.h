@@ -43,7 +43,25 @@ struct LTParams {
   float* W_out;
   double* loss;
   int64_t max_client_steps = 0;   // host bound on E * ceil(n_j / B) over the clients (0: unknown)
+  // fused evaluation (parallel split launches only): fuse_E extra workgroups on the CUs the
+  // groups leave idle evaluate W_start on the test set, partial sums into fuse_part[2E]
+  const float* fuse_phi = nullptr;
+  const int32_t* fuse_y = nullptr;
+  int fuse_n = 0, fuse_E = 0;
+  double* fuse_part = nullptr;
 };
+
+struct FuseEval {
+  const float* phi;
+  const int32_t* y;
+  int n, E;
+  double* part;
+};
+
+// workgroups a parallel split launch of this shape leaves idle (0: none, or not a split launch)
+int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained);
+// fs_eval's fold of nb partial pairs into out[0..1] (one workgroup)
+int eval_finalize_launch(const double* part, int nb, int n, double* out, hipStream_t st);
 
 // fs_local_train with a host bound on the steps of any client (the round plan knows the
 // client sizes; with the bound the split kernel tags its hand-offs by launch generation
@@ -51,7 +69,8 @@ struct LTParams {
 int local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                 const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E, float lr, float mu,
                 int prox, float lam, int reg, int chained, const float* d_W_start, float* d_W_out, double* d_loss,
-                int G, void* d_ws, int64_t ws_bytes, hipStream_t st, int64_t max_client_steps);
+                int G, void* d_ws, int64_t ws_bytes, hipStream_t st, int64_t max_client_steps,
+                const FuseEval* fuse = nullptr);
 
 // split-client launcher (local_train_split.hip): G workgroups per client
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);

@@ -133,6 +133,12 @@ __global__ __launch_bounds__(256) void eval_finalize(const double* __restrict__ 
   }
 }
 
+int eval_finalize_launch(const double* part, int nb, int n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(eval_finalize, dim3(1), dim3(256), 0, st, part, nb, n, out);
+  FS_LAUNCH_CHECK();
+  return FS_OK;
+}
+
 }  // namespace fs
 
 using namespace fs;

@@ -405,7 +405,7 @@ int fs::local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, co
                     const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E, float lr, float mu,
                     int prox, float lam, int reg, int chained, const float* d_W_start, float* d_W_out,
                     double* d_loss, int G, void* d_ws, int64_t ws_bytes, hipStream_t st,
-                    int64_t max_client_steps) {
+                    int64_t max_client_steps, const FuseEval* fuse) {
   FS_REQUIRE(N >= 1, "N must be >= 1");
   FS_REQUIRE(C >= 1 && C <= 32, "num_classes must be in [1, 32]");
   FS_REQUIRE(B >= 1 && B <= 64, "batch_size must be in [1, 64]");
@@ -414,6 +414,13 @@ int fs::local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, co
   FS_REQUIRE(d_phi && d_row_off && d_labels && d_perms && d_W_start && d_W_out && d_loss, "null pointer");
   LTParams P{d_phi, ld, d_row_off, d_labels, d_perms, d_order, N, C, B, E, lr, mu, lam,
              prox ? 1 : 0, reg ? 1 : 0, chained ? 1 : 0, d_W_start, d_W_out, d_loss, max_client_steps};
+  if (fuse && G > 1 && !chained) {
+    P.fuse_phi = fuse->phi;
+    P.fuse_y = fuse->y;
+    P.fuse_n = fuse->n;
+    P.fuse_E = fuse->E;
+    P.fuse_part = fuse->part;
+  }
   if (G > 1) {
     const int rc = launch_local_train_split(P, G, d_ws, ws_bytes, st);
     if (rc != FS_OK) return rc;

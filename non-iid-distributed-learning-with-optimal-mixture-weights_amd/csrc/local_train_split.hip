@@ -36,6 +36,7 @@
 #include <unordered_map>
 
 #include "common.h"
+#include "eval_rows.h"
 #include "lanes.h"
 
 namespace fs {
@@ -168,7 +169,15 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   // block -> (group, slice).  Chained: 8*G blocks are launched and those with
   // blockIdx % 8 == 0 take part (one XCD under round-robin placement).  Parallel: consecutive
   // linear ids on one XCD, so a group's partners mostly share an L2.  Speed only.
-  const int nb = gridDim.x;
+  // fused evaluation blocks (the last fuse_E blocks of a parallel launch): the test-set
+  // evaluation of W_start -- the previous round's global model -- on the CUs the groups leave
+  // idle, LDS from the (unused) image
+  const int nb = gridDim.x - P.fuse_E;
+  if ((int)blockIdx.x >= nb) {
+    eval_persistent<NWV>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
+                         xs_lds, P.fuse_part);
+    return;
+  }
   int lin;
   if (P.chained) {
     if (blockIdx.x % 8) return;
@@ -767,13 +776,25 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
     if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
   }
   const size_t lds = split_dyn_lds(RT, NT, G);
-  const int grid = P.chained ? 8 * G : ng * G;
+  if (P.fuse_E > 0 && (P.chained || NW != 8 || ng * G + P.fuse_E > cus || lds < sizeof(float) * NW * 16 * 17))
+    return fail(FS_EINVAL, "fs_local_train: no room for the fused evaluation");
+  const int grid = P.chained ? 8 * G : ng * G + P.fuse_E;
 #define FS_SPLIT_CASE(rt, g) \
   if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, NW, grid, lds, st); return FS_OK; }
   FS_SPLIT_CASE(2, 2) FS_SPLIT_CASE(2, 4) FS_SPLIT_CASE(2, 8) FS_SPLIT_CASE(2, 16)
   FS_SPLIT_CASE(1, 2) FS_SPLIT_CASE(1, 4) FS_SPLIT_CASE(1, 8) FS_SPLIT_CASE(1, 16)
 #undef FS_SPLIT_CASE
   return fail(FS_EUNSUPPORTED, "fs_local_train: no split kernel for this shape");
+}
+
+int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained) {
+  const int NT = (int)(ld >> 6);
+  if (chained || G < 2 || C > 16 || B > 32 || !split_fits(C, B, NT, G)) return 0;
+  const int cus = device_cus();
+  const int RT = split_rt(B);
+  const int NW = split_nw(RT, NT, G);
+  if (cus <= 0 || NW != 8) return 0;
+  return std::max(0, cus - split_groups(N, G, NW, 0, cus) * G);
 }
 
 }  // namespace fs

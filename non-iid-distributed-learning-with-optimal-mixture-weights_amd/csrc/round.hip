@@ -129,6 +129,8 @@ struct fs_plan {
   int64_t* d_pass = nullptr;                 // [2][P]: rows, offset of every pass (device replay)
   int64_t max_n = 0;
   int64_t max_client_steps = 0;       // E * ceil(max_j n_j / B)
+  int fuse_E = 0;                     // evaluation blocks a TRAIN launch can carry (0: none)
+  int eval_pending = -1;              // round whose evaluation rides on the next TRAIN launch
   hipStream_t copy = nullptr;
   hipEvent_t uploaded[2] = {nullptr, nullptr};
   hipEvent_t consumed[2] = {nullptr, nullptr};
@@ -250,6 +252,15 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
     int64_t mx = 0;
     for (int j = 0; j < d.N; ++j) mx = std::max(mx, d.h_n[j]);
     p->max_client_steps = std::max<int64_t>(1, (int64_t)d.E * ((mx + d.B - 1) / std::max(1, d.B)));
+  }
+  // FS_PHASE_EVAL_DEFER: a parallel split launch that leaves CUs idle evaluates the previous
+  // round's global model on them (FS_EVAL_FUSE=0 turns this off)
+  if (d.d_phi_t && d.n_t > 0 && d.d_labels_t && d.d_eval_ws && d.C <= 16 && d.G > 1 && !d.chained) {
+    const char* ev = std::getenv("FS_EVAL_FUSE");
+    if (!(ev && std::atoi(ev) == 0)) {
+      const int idle = fs::split_idle_cus(d.N, d.C, d.B, d.ld, d.G, 0);
+      p->fuse_E = (int)std::min<int64_t>(idle, (d.n_t + 15) / 16);
+    }
   }
   hipError_t e = hipSuccess;
   for (int s = 0; s < 2 && e == hipSuccess; ++s) {
@@ -463,6 +474,11 @@ extern "C" int fs_timer_destroy(void* ev) {
   return FS_OK;
 }
 
+extern "C" int fs_plan_eval_blocks(const fs_plan* p) {
+  FS_REQUIRE(p, "bad arguments");
+  return p->fuse_E;
+}
+
 extern "C" int fs_plan_shuffle_flush(fs_plan* p) {
   FS_REQUIRE(p, "bad arguments");
   return (p->chunk > 1 && p->fill_chunk >= 0) ? launch_chunk(p) : FS_OK;
@@ -508,11 +524,29 @@ static int run_shuffle_job(fs_plan* p, const int64_t* h_seeds, int t) {
   return FS_OK;
 }
 
+// the deferred evaluation of round p->eval_pending as a launch of its own
+static int flush_eval(fs_plan* p, hipStream_t st) {
+  if (p->eval_pending < 0) return FS_OK;
+  const fs_plan_desc& d = p->d;
+  const int te = p->eval_pending;
+  p->eval_pending = -1;
+  return fs_eval(d.d_phi_t, d.ld, d.d_labels_t, d.n_t, d.d_W_g, d.C, d.d_eval_hist + 2 * (int64_t)te, d.d_eval_ws, st);
+}
+
 extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const float* d_p_override, void* stream) {
   FS_REQUIRE(p && t >= 0, "bad arguments");
   const fs_plan_desc& d = p->d;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int s = t & 1;
+  // a deferred evaluation rides on this TRAIN launch (it reads W_g before the launch
+  // rewrites nothing but W_out); anything else that follows it runs it on its own first
+  fs::FuseEval fuse{d.d_phi_t, d.d_labels_t, (int)d.n_t, p->fuse_E, d.d_eval_ws};
+  const bool fused = (phases & FS_PHASE_TRAIN) && p->eval_pending >= 0 && p->fuse_E > 0;
+  if (p->eval_pending >= 0 && !fused) {
+    const int rc = flush_eval(p, st);
+    if (rc != FS_OK) return rc;
+  }
+  const int t_eval = p->eval_pending;
   if ((phases & FS_PHASE_TRAIN) && p->chunk > 1) {
     const int K = p->chunk, c = t / K, r = t % K, sc = c & 1;
     // a partly collected chunk (the last rounds of a run) is launched when first needed
@@ -529,7 +563,7 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
     const int rc = fs::local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[sc] + (int64_t)r * p->perm_len,
                                   d.d_order, d.N, d.C, d.B, d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g,
                                   d.d_W_out, d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, st,
-                                  p->max_client_steps);
+                                  p->max_client_steps, fused ? &fuse : nullptr);
     if (rc != FS_OK) return rc;
     if (r == p->slot_nrounds[sc] - 1) {            // the chunk's last round releases the slot
       FS_HIP(hipEventRecord(p->consumed[sc], st), "fs_plan_round");
@@ -551,10 +585,15 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
     const int rc = fs::local_train(d.d_phi, d.ld, d.d_row_off, d.d_labels, p->d_perm[s], d.d_order, d.N, d.C, d.B,
                                    d.E, lr, d.mu, d.prox, d.lam, d.reg, d.chained, d.d_W_g, d.d_W_out,
                                    d.d_loss_hist + (int64_t)t * d.N, d.G, d.d_ws, d.ws_bytes, st,
-                                   p->max_client_steps);
+                                   p->max_client_steps, fused ? &fuse : nullptr);
     if (rc != FS_OK) return rc;
     FS_HIP(hipEventRecord(p->consumed[s], st), "fs_plan_round");
     p->cons_recorded[s] = true;
+  }
+  if (fused) {
+    p->eval_pending = -1;
+    const int rc = fs::eval_finalize_launch(d.d_eval_ws, p->fuse_E, (int)d.n_t, d.d_eval_hist + 2 * (int64_t)t_eval, st);
+    if (rc != FS_OK) return rc;
   }
   if (phases & FS_PHASE_AGGREGATE) {
     const float* pw = d_p_override ? d_p_override : d.d_p;
@@ -566,6 +605,10 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
   }
   if (phases & FS_PHASE_EVAL) {
     FS_REQUIRE(d.d_phi_t && d.d_labels_t && d.d_eval_hist && d.d_eval_ws, "no test set");
+    if ((phases & FS_PHASE_EVAL_DEFER) && p->fuse_E > 0) {
+      p->eval_pending = t;                         // evaluated by the next TRAIN launch
+      return FS_OK;
+    }
     const int rc = fs_eval(d.d_phi_t, d.ld, d.d_labels_t, d.n_t, d.d_W_g, d.C, d.d_eval_hist + 2 * (int64_t)t,
                            d.d_eval_ws, stream);
     if (rc != FS_OK) return rc;

@@ -247,6 +247,13 @@ class RoundPlan:
         before the first ``shuffle``): no cross-stream wait between the rounds of a chunk."""
         _lib.check(_lib.lib().fs_plan_set_shuffle_chunk(self._h, int(rounds)), 'fs_plan_set_shuffle_chunk')
 
+    def eval_blocks(self):
+        """Evaluation workgroups a TRAIN launch carries for a deferred evaluation (0: none)."""
+        n = _lib.lib().fs_plan_eval_blocks(self._h)
+        if n < 0:
+            _lib.check(n, 'fs_plan_eval_blocks')
+        return n
+
     def flush(self):
         """Launch a partly collected chunk of shuffles (after a run's last round was prepared)."""
         _lib.check(_lib.lib().fs_plan_shuffle_flush(self._h), 'fs_plan_shuffle_flush')

@@ -202,6 +202,9 @@ class Federation:
             self.chunk = max(1, min(int(env_k) if env_k else 8, R))
             if self.chunk > 1:
                 self.plan.set_chunk(self.chunk)
+        # round t's test-set evaluation is deferred into round t+1's training launch when that
+        # launch leaves CUs idle (FS_EVAL_DEFER=0: an evaluation launch per round)
+        self.defer_eval = os.environ.get('FS_EVAL_DEFER', '0') != '0'
         self._prepared = 0              # next round whose shuffles are to be prepared
         self._train_done = None
         self.t = 0
@@ -237,6 +240,10 @@ class Federation:
             self._prepare_upto(2 * self.chunk if self.chunk > 1 else 1)
         self.lr = update_learning_rate(t, self.lr, self.R)
         P = _lib.PHASE_TRAIN, _lib.PHASE_AGGREGATE, _lib.PHASE_EVAL
+        if t + 1 < self.R and self.defer_eval:
+            # this round's evaluation rides on round t+1's training launch where that launch
+            # leaves CUs idle (fs_plan_round, FS_PHASE_EVAL_DEFER); same arithmetic per row
+            P = P[0], P[1], P[2] | _lib.PHASE_EVAL_DEFER
         ev = self.events
 
         def timed(name, fn):
@@ -299,6 +306,8 @@ class Federation:
     def results(self):
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""
         R, D = self.t, self.D
+        if 0 < R < self.R and self.defer_eval:
+            self.plan.round(R - 1, self.lr, 0)           # runs a deferred evaluation, if any
         self.trainer.check_errors()
         if self.mixture is not None:
             self.mixture.check_errors()

@@ -100,6 +100,50 @@ def test_dropin_shuffle_chunks(amd, monkeypatch, name, chunk):
     assert torch.equal(tr, tr8) and torch.equal(tl, tl8) and torch.equal(ta, ta8) and torch.equal(after, after8)
 
 
+@pytest.mark.parametrize('name', [c for c in LONG_CASES if 'seq' not in c])
+def test_dropin_deferred_eval(amd, monkeypatch, name):
+    """A round's evaluation carried by the next round's training launch (FS_PHASE_EVAL_DEFER, on
+    the CUs the client groups leave idle) gives the same test loss / accuracy as a launch of its
+    own: the same per-row arithmetic, only the double-precision sum order of the partials
+    differs (rtol 1e-12); the training itself is bitwise unchanged."""
+    d = load_long(name) if name in LONG_CASES else load(name)
+    monkeypatch.setenv('FS_EVAL_DEFER', '0')
+    (tr0, tl0, ta0), st0 = run_dropin(amd, d)
+    monkeypatch.setenv('FS_EVAL_DEFER', '1')
+    (tr1, tl1, ta1), st1 = run_dropin(amd, d)
+    assert np.array_equal(st0['W_rounds'], st1['W_rounds']) and torch.equal(tr0, tr1)
+    np.testing.assert_allclose(tl1.numpy(), tl0.numpy(), rtol=1e-12, atol=0)
+    assert torch.equal(ta0, ta1)
+
+
+def test_deferred_eval_uses_idle_cus(amd, monkeypatch):
+    """A parallel split plan with fewer client groups than CUs carries evaluation blocks, and
+    a deferred evaluation lands in the history only once the next TRAIN (or any call
+    without one) has run; FS_EVAL_FUSE=0 turns the fusion off."""
+    d = load_long([c for c in LONG_CASES if 'seq' not in c and 'fedamw' not in c][0])
+    monkeypatch.setenv('FS_EVAL_DEFER', '1')
+    Xs, ys = split_clients(d)
+    Xs = [torch.from_numpy(x) for x in Xs]
+    ys = [torch.from_numpy(y) for y in ys]
+    torch.manual_seed(int(d['torch_seed']))
+    fed = amd.tools.Federation('fedprox' if bool(d['prox']) else 'fedavg', Xs, ys, torch.from_numpy(d['X_test']),
+                               torch.from_numpy(d['y_test']), None, *positional(d)[:7], float(d['mu']), False,
+                               float(d['lam']), int(d['R']), 1e-3, 'parallel', verbose=False)
+    if fed.trainer.G < 2:
+        pytest.skip('not a split launch at this shape')
+    E = fed.plan.eval_blocks()
+    assert 0 < E <= 256 - fed.trainer.G
+    fed.eval_hist.fill_(-7.0)
+    fed.round()                                    # evaluation of round 0 deferred
+    torch.cuda.synchronize()
+    assert float(fed.eval_hist[0, 0]) == -7.0
+    fed.round()                                    # ... carried by round 1's training launch
+    torch.cuda.synchronize()
+    assert float(fed.eval_hist[0, 0]) != -7.0 and float(fed.eval_hist[1, 0]) == -7.0
+    tr, tl, ta = fed.results()                     # results() runs the pending one
+    assert np.isfinite(tl[:2].numpy()).all() and float(fed.eval_hist[1, 0]) != -7.0
+
+
 def test_dropin_consumes_rng_like_reference(amd):
     """After the call, the global generator must be where the reference left it."""
     d = load('fedprox_seq')
