@@ -204,7 +204,7 @@ class Federation:
                 self.plan.set_chunk(self.chunk)
         # round t's test-set evaluation is deferred into round t+1's training launch when that
         # launch leaves CUs idle (FS_EVAL_DEFER=0: an evaluation launch per round)
-        self.defer_eval = os.environ.get('FS_EVAL_DEFER', '0') != '0'
+        self.defer_eval = os.environ.get('FS_EVAL_DEFER', '1') != '0'
         self._prepared = 0              # next round whose shuffles are to be prepared
         self._train_done = None
         self.t = 0
