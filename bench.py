@@ -1,52 +1,58 @@
 #!/usr/bin/env python3
-"""Benchmark: client-rounds/s of the federated round on MI355X (BASELINE.json config 2).
+"""Benchmark: client-rounds/s of the federated round on MI355X (BASELINE.json configs 2-5).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo fedavg|fedprox|fedamw]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [...]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
-One step = one federated round with parallel clients (every client of the round
-trains from the global model): per-client local SGD (fs_local_train), weighted
-aggregation (fs_aggregate; + one RCCL all-reduce of the C x D partial aggregate
-when N > 1), test evaluation (fs_eval), and the host's RNG replay of every shuffle.
-Workload per GPU = config 2: 100 non-IID (label-skewed) a9a-shaped clients x 512
-rows, random-feature dim 2048, 10 classes, E = 2, B = 32, 10,000 test rows.
-Weak scaling: each rank owns 100 clients, so the job simulates 100 * N clients.
-Inputs are resident in HBM before the timed region; `value` = all ranks' client
-rounds / the max-over-ranks wall time of the K timed rounds.
+Launch.  ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment: this process
+starts N worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per
+GPU) before it makes any GPU call, relays rank 0's JSON line and exits non-zero if any
+worker fails.  Under torchrun (WORLD_SIZE set) it is one of those workers.  A worker whose
+LOCAL_RANK has no GPU fails; only the explicit FS_BENCH_BACKEND=gloo rehearsal (several
+ranks sharing the visible GPUs, host-staged gloo collectives) wraps ranks onto devices.
+
+One step = one federated round with parallel clients (every client of the round trains
+from the global model): per-client local SGD (fs_local_train), weighted aggregation
+(fs_aggregate; + one RCCL all-reduce of the C x D partial aggregate when N > 1), test
+evaluation (fs_eval) and the device replay of every shuffle.  The headline workload
+(``value``) is BASELINE config 2 per GPU: 100 non-IID (label-skewed) a9a-shaped clients x
+512 rows, random-feature dim 2048, 10 classes, E = 2, B = 32, 10,000 test rows; weak
+scaling: each rank owns 100 clients.  Inputs are resident in HBM before the timed region;
+``value`` = all ranks' client-rounds / the max-over-ranks wall time of the K timed rounds.
 
 Extra objects on the JSON line:
+  dist          the process group as it ran: backend, world size, distinct devices, and one
+                checked all-reduce (sum of rank+1 over the ranks).
   roofline      fs_local_train (the dominant kernel): algorithmic HBM bytes per launch
                 (4*E*sum(n_j)*D + 8*E*sum(n_j) + 8*N*C*D) / mean launch time
-                from HIP events on the launch stream, against 8 TB/s; `traffic` = PMC HBM
-                bytes per launch from profiles/traffic_local_train_<config>.json (rocprofv3
-                FETCH_SIZE*2 + WRITE_SIZE), used only when its `source_rev` equals the
-                revision of the kernel sources being run (_lib.source_revision()), else null.
-  cpu_baseline  the CPU oracle (oracle/fedsim_oracle.py, numpy restatement of the
-                reference round) timed on this host on whole rounds of the same workload.
-  fedamw        (config 2, one GPU) the other half of config 2 -- "FedAvg vs optimal
-                mixture weights": FedAMW rounds on the same clients plus 128 validation
-                rows each (tools.py:413-463): ms per round, the p-solve's sequential steps/s
-                and its bytes/s against 8 TB/s (4*R*N*C*n_v bytes of Z per round), the Z-GEMM's
-                TFLOP/s against the fp32 MFMA peak (2*N*C*D*n_v flop per round).
+                from HIP events on the launch stream, against 8 TB/s; ``traffic`` = PMC HBM
+                bytes per launch and ``mfma_busy`` = the MFMA pipe's busy fraction, both from
+                profiles/traffic_local_train_<config>.json, used only when its ``source_rev``
+                equals the revision of the kernel sources being run (_lib.source_revision()).
+  cpu_baseline  the CPU oracle (oracle/fedsim_oracle.py, numpy restatement of the reference
+                round) timed on this host (rank 0, N = 1 only) on a bounded sample.
+  fedamw        (config 2, one GPU) the other half of config 2 -- "FedAvg vs optimal mixture
+                weights": FedAMW rounds on the same clients plus 128 validation rows each.
+  config4 / config3 / config5
+                (default run) the >= 1000-client BASELINE configs, each with its own rounds,
+                ms_per_round, client-rounds/s, roofline and cpu_baseline; config 5 adds the
+                p-solve's steps/s, bytes/s and PMC traffic.
 Config 5 is BASELINE's 1000 clients over all GPUs (strong scaling: 1000/N clients per GPU);
 the others keep their per-GPU share fixed (weak scaling).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
-import torch
-import torch.distributed as tdist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import fedamw_amd  # noqa: E402
-from fedamw_amd import data as fdata  # noqa: E402
-from fedamw_amd.functions import tools  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3   # dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md
@@ -62,11 +68,13 @@ PRESETS = {
     5: dict(algo='fedamw', clients=1000, rows=128, D=16384, C=10, test=10000, shape='a9a'),
 }
 STRONG = {5}
+# the extra legs of the default run: (config, timed rounds, warmup rounds)
+LEGS = ((4, 10, 2), (3, 5, 1), (5, 2, 1))
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='GPUs (ranks); default WORLD_SIZE or 1')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', type=int, default=2, choices=sorted(PRESETS),
@@ -80,12 +88,14 @@ def parse():
     ap.add_argument('--shape', choices=['a9a', 'covtype'])
     ap.add_argument('--rounds', type=int, help="the algorithm's `round` argument (LR schedule; FedAMW's inner "
                                                 'p-SGD epochs per round); default 100 = the reference default')
-    ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the CPU baseline sample')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0, help='budget of the headline CPU baseline sample')
+    ap.add_argument('--leg-cpu-seconds', type=float, default=3.0, help='budget of each extra leg\'s CPU sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--host-shuffle', action='store_true', help='replay shuffles on host threads, not the GPU')
     ap.add_argument('--no-fedamw-leg', action='store_true', help='skip the FedAMW object of the config-2 line')
     ap.add_argument('--fedamw-rounds', type=int, default=2, help='timed FedAMW rounds of the config-2 leg')
-    a = ap.parse_args()
+    ap.add_argument('--no-legs', action='store_true', help='skip the config 3/4/5 objects of the default line')
+    a = ap.parse_args(argv)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -95,41 +105,107 @@ def parse():
     return a
 
 
-def cpu_baseline(d, args, budget):
-    """Whole FedAvg rounds of the same workload through the numpy oracle (rank 0 only)."""
-    from oracle import fedsim_oracle as O
-    from threadpoolctl import threadpool_info
-    Xs = [x.cpu().numpy() for x in d['X_train']]
-    ys = [y.cpu().numpy() for y in d['y_train']]
-    Xt, yt = d['X_test'].cpu().numpy(), d['y_test'].cpu().numpy()
-    p = O._weights(ys)
-    W = O.mlp_init(args.D, args.C)
-    state = torch.get_rng_state()
-    torch.manual_seed(1234)
-    rounds, clients_done = 0, 0
-    t0 = time.perf_counter()
-    while True:
-        Ws = []
-        for X, y in zip(Xs, ys):
-            Wj, _ = O.train_client(X, y, W, 0.5, 2, 32, args.algo == 'fedprox', 5e-4, False, 0.0)
-            Ws.append(Wj)
-            clients_done += 1
-        W = O.aggregate(Ws, p)
-        O.test_eval(Xt, yt, W)
-        rounds += 1
-        el = time.perf_counter() - t0
-        if el >= budget:
+# --------------------------------------------------------------------------------------------
+# launcher (no GPU call in this process)
+# --------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn(n, cmd=None):
+    """Start n worker processes of this script (one per GPU; ``cmd`` overrides the command,
+    for tests), relay rank 0's stdout, and return the exit code: 0 only if every worker
+    exited 0.  A failed worker ends the others (they would wait forever in a collective)."""
+    cmd = cmd or [sys.executable, '-u', os.path.abspath(__file__)] + sys.argv[1:]
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+
+    def relay(pipe):
+        for line in pipe:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p for p in procs if p.poll() not in (None, 0)]
+        if bad:
+            rc = bad[0].returncode
+            print('bench: worker pid %d exited %d; stopping the others' % (bad[0].pid, rc), file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 20
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
             break
-    torch.set_rng_state(state)
-    threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
-    return {'value': clients_done / el, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
-            'sample': '%d whole round(s) (%d clients x %d rows, D=%d, C=%d, E=2, B=32, aggregate + %d-row test eval) '
-                      'of the numpy oracle, %.1f s' % (rounds, len(Xs), args.rows, args.D, args.C, len(yt), el)}
+        time.sleep(0.2)
+    th.join(timeout=5)
+    for p in procs:
+        if p.returncode not in (0, None) and rc == 0:
+            rc = p.returncode
+    return rc if rc >= 0 else 128 - rc
 
 
-def load_traffic(tag, kernel='local_train'):
-    """PMC HBM bytes per launch measured for exactly this workload AND these kernel sources
-    (profiles/traffic_<kernel>_<tag>.json with a matching source_rev), else None."""
+# --------------------------------------------------------------------------------------------
+# worker
+# --------------------------------------------------------------------------------------------
+def setup_rank(args):
+    """Device + process group of this worker.  Returns (ws, rank, dev, dist_info)."""
+    import torch
+    import torch.distributed as tdist
+    ws = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    if args.gpus is not None and args.gpus != ws:
+        raise SystemExit('bench: --gpus %d but WORLD_SIZE=%d' % (args.gpus, ws))
+    backend = os.environ.get('FS_BENCH_BACKEND', 'nccl') if ws > 1 else None
+    if backend not in (None, 'nccl', 'gloo'):
+        raise SystemExit('bench: FS_BENCH_BACKEND must be nccl or gloo')
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = torch.cuda.device_count()
+    if backend == 'gloo':
+        local = local % max(1, ndev)          # rehearsal only: ranks may share the visible GPUs
+    elif local >= ndev:
+        raise SystemExit('bench: LOCAL_RANK %d has no GPU (%d visible)' % (local, ndev))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    info = {'backend': None, 'world_size': 1, 'devices': 1}
+    if ws > 1:
+        if backend == 'nccl':
+            tdist.init_process_group('nccl', device_id=dev)
+        else:
+            tdist.init_process_group('gloo')
+        t = torch.tensor([float(rank + 1)], device=dev if backend == 'nccl' else 'cpu')
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+        want = ws * (ws + 1) / 2.0
+        if float(t.item()) != want:
+            raise SystemExit('bench: all-reduce sanity check gave %r, expected %r' % (float(t.item()), want))
+        ids = [None] * ws
+        tdist.all_gather_object(ids, (socket.gethostname(), torch.cuda.get_device_properties(dev).uuid
+                                      if hasattr(torch.cuda.get_device_properties(dev), 'uuid') else local))
+        info = {'backend': tdist.get_backend(), 'world_size': tdist.get_world_size(),
+                'devices': len(set(str(i) for i in ids)), 'allreduce_check': float(t.item()),
+                'rehearsal': backend == 'gloo'}
+    return ws, rank, dev, info
+
+
+def load_record(tag, kernel):
+    """PMC record (HBM bytes, MFMA busy) measured for exactly this workload AND these kernel
+    sources (profiles/traffic_<kernel>_<tag>.json with a matching source_rev), else None."""
     from fedamw_amd import _lib
     path = os.path.join(ROOT, 'profiles', 'traffic_%s_%s.json' % (kernel, tag))
     if not os.path.exists(path):
@@ -142,9 +218,77 @@ def load_traffic(tag, kernel='local_train'):
     return rec, 'PMC %s' % rec.get('source', '')
 
 
+def phase_ms(events, name):
+    v = [a.elapsed_time(b) for n, a, b in (events or []) if n == name]
+    return float(np.mean(v)) if v else None
+
+
+def _np(x):
+    return x.detach().cpu().numpy()
+
+
+def cpu_baseline(d, wl, budget, fedamw, rounds_R):
+    """The numpy oracle on this host's cores, on a bounded sample of the same workload:
+    local training of as many clients as fit ~60 % of ``budget`` (whole rounds when they all
+    fit), the aggregate and the test evaluation; FedAMW adds the Z GEMM on a sample of the
+    validation rows and a sample of the round's p-SGD steps.  Extrapolated to client-rounds/s."""
+    import torch
+    from oracle import fedsim_oracle as O
+    from threadpoolctl import threadpool_info
+    N, D, C = len(d['X_train']), wl['D'], wl['C']
+    state = torch.get_rng_state()
+    torch.manual_seed(1234)
+    W = O.mlp_init(D, C)
+    t0 = time.perf_counter()
+    Ws, t_train = [], 0.0
+    for j in range(N):
+        X, y = _np(d['X_train'][j]), _np(d['y_train'][j])
+        a = time.perf_counter()
+        Wj, _ = O.train_client(X, y, W, 0.5, 2, 32, wl['algo'] == 'fedprox', 5e-4, fedamw, 1e-5)
+        t_train += time.perf_counter() - a
+        Ws.append(Wj)
+        if time.perf_counter() - t0 > 0.6 * budget:
+            break
+    k = len(Ws)
+    p = np.full(k, 1.0 / N, dtype=np.float32)
+    a = time.perf_counter()
+    O.aggregate(Ws, p)
+    t_agg = (time.perf_counter() - a) * N / k
+    Xt, yt = _np(d['X_test']), _np(d['y_test'])
+    a = time.perf_counter()
+    O.test_eval(Xt, yt, Ws[-1])
+    t_eval = time.perf_counter() - a
+    t_round = t_train * N / k + t_agg + t_eval
+    sample = ('%d of %d clients\' local training (%d rows, D=%d, C=%d, E=2, B=32) + aggregate + %d-row test eval'
+              % (k, N, len(d['y_train'][0]), D, C, len(yt)))
+    if fedamw:
+        nv = int(d['y_val'].numel()) if torch.is_tensor(d['y_val']) else len(d['y_val'])
+        sv = min(nv, 512)
+        Xv = _np(d['X_val'][:sv])
+        a = time.perf_counter()
+        np.einsum('ncd,vd->ncv', np.stack(Ws).astype(np.float32), Xv, optimize=True)
+        t_z = (time.perf_counter() - a) * (N / k) * (nv / sv)
+        steps = rounds_R * ((nv + 15) // 16)
+        Zs = np.random.RandomState(0).standard_normal((N, C, 16 * 64)).astype(np.float32) * 0.1
+        yv = np.random.RandomState(1).randint(0, C, 16 * 64)
+        a = time.perf_counter()
+        O.mixture_solve_z(Zs, yv, np.full(N, 1.0 / N, np.float32), None, 1e-3, 1, 16)
+        t_solve = (time.perf_counter() - a) / 64 * steps
+        t_round += t_z + t_solve
+        sample += ('; FedAMW: Z GEMM on %d of %d validation rows, 64 of the round\'s %d p-SGD steps (N=%d)'
+                   % (sv, nv, steps, N))
+    el = time.perf_counter() - t0
+    torch.set_rng_state(state)
+    threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
+    return {'value': N / t_round, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
+            'sample': sample + ' of the numpy oracle, %.1f s, extrapolated to whole rounds' % el}
+
+
 def pool_validation(d, ws, dev):
     """Every rank's clients contribute their validation rows; the pooled set (exp.py:92-99)
     is identical on every rank: one all-gather of the per-rank blocks (equal sizes)."""
+    import torch
+    import torch.distributed as tdist
     Xv, yv = d['X_val'], d['y_val']
     if ws == 1:
         return Xv, yv
@@ -155,19 +299,17 @@ def pool_validation(d, ws, dev):
     return bx, by
 
 
-def phase_ms(events, name):
-    v = [a.elapsed_time(b) for n, a, b in (events or []) if n == name]
-    return float(np.mean(v)) if v else None
-
-
-def fedamw_leg(d, args, dev, rounds, warmup=1):
+def fedamw_leg(d, wl, dev, R, rounds, warmup=1):
     """The FedAMW half of config 2 on the same clients (one GPU)."""
-    N, E, B, R = args.clients, 2, 32, args.rounds
+    import torch
+    import fedamw_amd
+    from fedamw_amd.functions import tools
+    N, E, B = wl['clients'], 2, 32
     vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(d['X_val'], d['y_val']), batch_size=16,
                                      shuffle=True)
     torch.manual_seed(100)
     fed = tools.Federation('fedamw', d['X_train'], d['y_train'], d['X_test'], d['y_test'], vl, 'classification',
-                           args.C, args.D, 0.5, E, B, False, 0.0, True, 1e-5, max(R, warmup + rounds), 1e-3,
+                           wl['C'], wl['D'], 0.5, E, B, False, 0.0, True, 1e-5, max(R, warmup + rounds), 1e-3,
                            'parallel', verbose=False)
     for _ in range(warmup):
         fed.round()
@@ -182,136 +324,202 @@ def fedamw_leg(d, args, dev, rounds, warmup=1):
     nv = fed.mixture.nv
     steps = R * ((nv + 15) // 16)
     z_ms, solve_ms, train_ms = (phase_ms(fed.events, k) for k in ('z', 'solve', 'train'))
-    z_flop = 2.0 * N * args.C * args.D * nv
-    solve_bytes = 4.0 * R * N * args.C * nv
+    z_flop = 2.0 * N * wl['C'] * wl['D'] * nv
+    solve_bytes = 4.0 * R * N * wl['C'] * nv
+    rec, note = load_record('c2_fedamw', 'mix_solve')
     return {'ms_per_round': 1e3 * el / rounds, 'client_rounds_per_s': N * rounds / el,
             'train_ms': train_ms, 'z_gemm_ms': z_ms, 'z_gemm_tflops': z_flop / (z_ms * 1e-3) / 1e12,
             'z_gemm_frac_mfma_f32': z_flop / (z_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
             'p_solve_ms': solve_ms, 'p_solve_steps': steps, 'p_solve_us_per_step': 1e3 * solve_ms / steps,
             'p_solve_steps_per_s': steps / (solve_ms * 1e-3), 'p_solve_gbs': solve_bytes / (solve_ms * 1e-3) / 1e9,
             'p_solve_frac_hbm': solve_bytes / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            'p_solve_traffic': (rec or {}).get('bytes_per_launch'), 'p_solve_traffic_note': note,
             'p_solver': fedamw_amd._lib.SOLVER_NAMES.get(fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
             'n_val': nv, 'inner_epochs': R, 'rounds_timed': rounds}
 
 
-def main():
-    args = parse()
-    ws = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    # (ranks wrap onto the visible devices and FS_BENCH_BACKEND=gloo swaps RCCL out: only to
-    # rehearse the multi-rank path on a one-GPU box; the driver's runs are one rank per GPU)
-    local = int(os.environ.get('LOCAL_RANK', '0')) % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
-    if ws > 1:
-        backend = os.environ.get('FS_BENCH_BACKEND', 'nccl')
-        if backend == 'nccl':
-            tdist.init_process_group('nccl', device_id=dev)
-        else:
-            tdist.init_process_group(backend)
-    strong = args.config in STRONG and not args.custom
-    N_loc = args.clients // ws if strong else args.clients
+def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuffle=False, custom=False,
+                 fedamw_leg_rounds=0):
+    """One BASELINE workload: set up (untimed), ``warmup`` rounds, ``steps`` timed rounds
+    bracketed by barrier + synchronize, max over ranks.  Returns the workload's line fields."""
+    import torch
+    import torch.distributed as tdist
+    from fedamw_amd import data as fdata
+    from fedamw_amd import dist as fdist
+    from fedamw_amd.functions import tools
+    cfg = wl['config']
+    strong = cfg in STRONG and not custom
+    N_loc = wl['clients'] // ws if strong else wl['clients']
     if N_loc < 1:
         raise SystemExit('bench: fewer clients than GPUs')
     E, B = 2, 32
-    fedamw = args.algo == 'fedamw'
-    leg = (args.config == 2 and not args.custom and not fedamw and ws == 1 and not args.no_fedamw_leg)
-    n_val = 128 if leg else (args.rows // 4 if fedamw else 0)
+    algo = wl['algo']
+    fedamw = algo == 'fedamw'
+    leg = fedamw_leg_rounds > 0
+    n_val = 128 if leg else (wl['rows'] // 4 if fedamw else 0)
     # every rank synthesises its own clients (seed 1000 + rank); the pooled validation set of
     # FedAMW is all-gathered so that every rank solves the same p
-    d = fdata.federated(N_loc, args.rows, args.D, args.C, args.test, n_val=n_val, shape=args.shape,
+    d = fdata.federated(N_loc, wl['rows'], wl['D'], wl['C'], wl['test'], n_val=n_val, shape=wl['shape'],
                         seed=1000 + rank, device=dev)
     # the job's client list: Federation shards clients by LPT; this rank's synthetic clients are
     # placed at the positions it will own, the other ranks' rows are never touched here.
-    from fedamw_amd import dist as fdist
     N_all = N_loc * ws
-    shards = fdist.shard_lpt(fdist.client_work(np.full(N_all, args.rows), E, B), ws)
+    shards = fdist.shard_lpt(fdist.client_work(np.full(N_all, wl['rows']), E, B), ws)
     Xs = [None] * N_all
-    ys = [torch.zeros(args.rows, dtype=torch.int64)] * N_all      # other ranks' clients: lengths only
+    ys = [torch.zeros(wl['rows'], dtype=torch.int64)] * N_all      # other ranks' clients: lengths only
     for k, j in enumerate(shards[rank]):
         Xs[j], ys[j] = d['X_train'][k], d['y_train'][k]
-    lr, mu = 0.5, (5e-4 if args.algo == 'fedprox' else 0.0)
-    R = max(args.rounds, args.warmup + args.steps)
+    lr, mu = 0.5, (5e-4 if algo == 'fedprox' else 0.0)
+    R = max(R_arg, warmup + steps)
     vl = None
     if fedamw:
         Xv, yv = pool_validation(d, ws, dev)
         vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(Xv, yv), batch_size=16, shuffle=True)
     torch.manual_seed(100)
-    fed = tools.Federation(args.algo, Xs, ys, d['X_test'], d['y_test'], vl, 'classification', args.C, args.D, lr,
-                           E, B, args.algo == 'fedprox', mu, fedamw, 1e-5, R, 1e-3,
-                           'parallel', verbose=False, shuffle_device=not args.host_shuffle)
+    fed = tools.Federation(algo, Xs, ys, d['X_test'], d['y_test'], vl, 'classification', wl['C'], wl['D'], lr,
+                           E, B, algo == 'fedprox', mu, fedamw, 1e-5, R, 1e-3,
+                           'parallel', verbose=False, shuffle_device=not host_shuffle)
     assert len(fed.mine) == N_loc
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         fed.round()
     torch.cuda.synchronize()
-    fed.events = None if os.environ.get('FS_BENCH_NO_EVENTS') == '1' else []   # (diagnostic A/B)
+    fed.events = []
     if ws > 1:
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    host_t = []
-    for _ in range(args.steps):
-        h0 = time.perf_counter()
+    for _ in range(steps):
         fed.round()
-        host_t.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     if ws > 1:
         tdist.barrier()
     el = time.perf_counter() - t0
-    if os.environ.get('FS_BENCH_HOST_TIMES') == '1':     # (diagnostic: host enqueue time per round)
-        print('host us per round() call: mean %.1f min %.1f max %.1f; wall per round %.1f'
-              % (1e6 * np.mean(host_t), 1e6 * np.min(host_t), 1e6 * np.max(host_t), 1e6 * el / args.steps),
-              file=sys.stderr, flush=True)
     if ws > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], device=dev if tdist.get_backend() == 'nccl' else 'cpu', dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         el = float(t.item())
     lt_ms = phase_ms(fed.events, 'train')
     tr, tl, ta = fed.results()
     n_rows = int(fed.feats.rows)
-    alg_bytes = 4.0 * E * n_rows * args.D + 8.0 * E * n_rows + 8.0 * N_loc * args.C * args.D
+    alg_bytes = 4.0 * E * n_rows * wl['D'] + 8.0 * E * n_rows + 8.0 * N_loc * wl['C'] * wl['D']
     achieved = alg_bytes / (lt_ms * 1e-3) / 1e9 if lt_ms else float('nan')
-    tag = 'c%d%s' % (args.config, '' if args.algo == PRESETS[args.config]['algo'] else '_' + args.algo)
-    traffic, tnote = (None, 'custom workload') if args.custom else load_traffic(tag)
+    tag = 'c%d%s' % (cfg, '' if algo == PRESETS[cfg]['algo'] else '_' + algo)
+    rec, tnote = (None, 'custom workload') if custom else load_record(tag, 'local_train')
     total = N_loc * ws
     out = {
-        'metric': 'client-rounds/sec (whole node)',
-        'value': total * args.steps / el,
-        'unit': 'client-rounds/s',
-        'n_gpus': ws,
-        'steps': args.steps,
-        'warmup': args.warmup,
-        'ms_per_step': 1e3 * el / args.steps,
-        'higher_is_better': True,
+        'value': total * steps / el,
+        'ms_per_step': 1e3 * el / steps,
+        'steps': steps,
         'scaling': 'strong' if strong else 'weak',
-        'vs_baseline': None,
-        'dtype': 'f32',
-        'data': 'synthetic (%s-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)' % args.shape,
-        'config': {'workload': '%s: %s, %d clients%s x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, '
-                               'round=%d, parallel clients'
-                               % ('custom' if args.custom else 'config %d' % args.config, args.algo, total,
-                                  '' if strong or ws == 1 else ' (%d/GPU)' % N_loc, args.rows, args.D, args.C, E, B,
-                                  args.test, R),
-                   'algo': args.algo, 'clients_total': total, 'clients_per_gpu': N_loc, 'rows_per_client': args.rows,
-                   'D': args.D, 'C': args.C, 'epochs': E, 'batch': B, 'test_rows': args.test,
+        'workload': '%s: %s, %d clients%s x %d rows, RFF D=%d, C=%d, E=%d, B=%d, %d test rows, round=%d, '
+                    'parallel clients' % ('custom' if custom else 'config %d' % cfg, algo, total,
+                                          '' if strong or ws == 1 else ' (%d/GPU)' % N_loc, wl['rows'], wl['D'],
+                                          wl['C'], E, B, wl['test'], R),
+        'config': {'algo': algo, 'clients_total': total, 'clients_per_gpu': N_loc, 'rows_per_client': wl['rows'],
+                   'D': wl['D'], 'C': wl['C'], 'epochs': E, 'batch': B, 'test_rows': wl['test'],
                    'parallelism': 'clients%d' % ws},
         'roofline': {'kernel': 'fs_local_train', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                     'traffic': (traffic or {}).get('bytes_per_launch'), 'traffic_note': tnote,
+                     'traffic': (rec or {}).get('bytes_per_launch'), 'traffic_note': tnote,
+                     'mfma_busy': (rec or {}).get('mfma_busy'),
                      'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes, 'group_width': fed.trainer.G},
         'final_test_acc': float(ta[fed.t - 1]),
     }
     if fedamw:
-        out['fedamw'] = {'z_gemm_ms': phase_ms(fed.events, 'z'), 'z_allgather_ms': phase_ms(fed.events, 'z_allgather'),
-                         'p_solve_ms': phase_ms(fed.events, 'solve'), 'n_val': fed.mixture.nv}
+        nv = fed.mixture.nv
+        p_steps = R * ((nv + 15) // 16)
+        s_ms = phase_ms(fed.events, 'solve')
+        z_ms = phase_ms(fed.events, 'z')
+        sbytes = 4.0 * R * fed.mixture.N * wl['C'] * nv
+        zflop = 2.0 * fed.mixture.N * wl['C'] * wl['D'] * nv / ws
+        prec, pnote = (None, 'custom workload') if custom or ws > 1 else load_record(tag, 'mix_solve')
+        out['fedamw'] = {'z_gemm_ms': z_ms, 'z_gemm_tflops': zflop / (z_ms * 1e-3) / 1e12 if z_ms else None,
+                         'z_allgather_ms': phase_ms(fed.events, 'z_allgather'),
+                         'p_solve_ms': s_ms, 'n_val': nv, 'p_solve_steps': p_steps,
+                         'p_solve_us_per_step': 1e3 * s_ms / p_steps if s_ms else None,
+                         'p_solve_steps_per_s': p_steps / (s_ms * 1e-3) if s_ms else None,
+                         'p_solve_gbs': sbytes / (s_ms * 1e-3) / 1e9 if s_ms else None,
+                         'p_solve_frac_hbm': sbytes / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if s_ms else None,
+                         'p_solve_alg_bytes': sbytes,
+                         'p_solve_traffic': (prec or {}).get('bytes_per_launch'), 'p_solve_traffic_note': pnote,
+                         'p_solver': _solver_name()}
     if leg:
-        out['fedamw'] = fedamw_leg(d, args, dev, args.fedamw_rounds)
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(d, args, args.cpu_seconds)
+        out['fedamw'] = fedamw_leg(d, wl, dev, R_arg, fedamw_leg_rounds)
+    if rank == 0 and ws == 1 and cpu_seconds > 0:
+        out['cpu_baseline'] = cpu_baseline(d, wl, cpu_seconds, fedamw, R_arg)
+    del fed, d, Xs, ys, vl
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def _solver_name():
+    from fedamw_amd import _lib
+    return _lib.SOLVER_NAMES.get(_lib.lib().fs_mix_solve_last_mode(), '?')
+
+
+def worker(args):
+    import torch
+    import torch.distributed as tdist
+    import fedamw_amd  # noqa: F401
+    ws, rank, dev, dinfo = setup_rank(args)
+    wl = {k: getattr(args, k) for k in ('algo', 'clients', 'rows', 'D', 'C', 'test', 'shape')}
+    wl['config'] = args.config
+    headline = (args.config == 2 and not args.custom)
+    leg_rounds = args.fedamw_rounds if (headline and args.algo == 'fedavg' and ws == 1
+                                        and not args.no_fedamw_leg) else 0
+    cpu_s = 0.0 if args.no_cpu_baseline else args.cpu_seconds
+    main = run_workload(wl, ws, rank, dev, args.steps, args.warmup, args.rounds, cpu_s, args.host_shuffle,
+                        args.custom, leg_rounds)
+    out = {
+        'metric': 'client-rounds/sec (whole node)',
+        'value': main['value'],
+        'unit': 'client-rounds/s',
+        'n_gpus': dinfo['world_size'],
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': main['ms_per_step'],
+        'higher_is_better': True,
+        'scaling': main['scaling'],
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic (%s-shaped raw rows -> RFF, label-skewed Dirichlet(0.1) clients)' % args.shape,
+        'config': dict(workload=main['workload'], **main['config']),
+        'dist': dinfo,
+        'roofline': main['roofline'],
+        'final_test_acc': main['final_test_acc'],
+    }
+    for k in ('fedamw', 'cpu_baseline'):
+        if k in main:
+            out[k] = main[k]
+    if headline and not args.no_legs:
+        for cfg, k, w in LEGS:
+            lw = dict(PRESETS[cfg], config=cfg)
+            t0 = time.perf_counter()
+            r = run_workload(lw, ws, rank, dev, k, w, 100, 0.0 if args.no_cpu_baseline else args.leg_cpu_seconds)
+            obj = {'workload': r['workload'], 'value': r['value'], 'unit': 'client-rounds/s',
+                   'ms_per_round': r['ms_per_step'], 'rounds_timed': k, 'warmup': w, 'scaling': r['scaling'],
+                   'roofline': r['roofline'], 'final_test_acc': r['final_test_acc'],
+                   'leg_wall_s': time.perf_counter() - t0}
+            for key in ('fedamw', 'cpu_baseline'):
+                if key in r:
+                    obj[key] = r[key]
+            out['config%d' % cfg] = obj
+            if rank == 0:
+                print('bench: config %d leg %.1f s, %.0f client-rounds/s' % (cfg, obj['leg_wall_s'], obj['value']),
+                      file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:
+        tdist.barrier()
         tdist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if (args.gpus or 1) > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn(args.gpus))       # before any GPU call: this process only relays
+    worker(args)
 
 
 if __name__ == '__main__':

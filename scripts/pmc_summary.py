@@ -65,6 +65,15 @@ def main():
                'lds_active_cycles': mean(k, 'SQ_LDS_IDX_ACTIVE'),
                'mfma_busy_cycles': mean(k, 'SQ_VALU_MFMA_BUSY_CYCLES'),
                'grbm_gui_active': mean(k, 'GRBM_GUI_ACTIVE')}
+        # MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES is summed over every SIMD of the chip
+        # (32 per v_mfma_f32_16x16x4_f32 = its issue cycles on one SIMD; checked against the
+        # launch's MFMA count), GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md, DVFS
+        # item) -> busy / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) = the fraction of the chip's
+        # MFMA issue cycles spent in MFMAs during the launch
+        if rec['mfma_busy_cycles'] is not None and rec['grbm_gui_active']:
+            rec['mfma_busy'] = rec['mfma_busy_cycles'] / (1024.0 * rec['grbm_gui_active'] / 8.0)
+            rec['mfma_busy_note'] = ('SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): '
+                                     'chip-wide MFMA pipe busy fraction over the launch')
         name = kname.replace('_kernel', '')
         with open(os.path.join(ROOT, 'profiles', 'traffic_%s_%s.json' % (name, tag)), 'w') as fh:
             json.dump(rec, fh, indent=1)

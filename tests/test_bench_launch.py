@@ -1,0 +1,62 @@
+"""bench.py's multi-rank launcher on CPU: ``--gpus N`` starts N workers with the
+torch.distributed environment, relays rank 0's line, and fails when a worker fails."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+WORKER = r'''
+import json, os, sys
+import torch, torch.distributed as tdist
+r, ws = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+assert os.environ['MASTER_ADDR'] == '127.0.0.1' and os.environ['LOCAL_RANK'] == str(r)
+tdist.init_process_group('gloo')
+t = torch.tensor([float(r + 1)])
+tdist.all_reduce(t)
+if r == 0:
+    print(json.dumps({'world_size': tdist.get_world_size(), 'sum': float(t.item())}), flush=True)
+tdist.destroy_process_group()
+sys.exit(int(os.environ.get('FAIL_RANK', '-1') == str(r)) * 3)
+'''
+
+
+def test_spawn_relays_rank0(tmp_path, capfd):
+    w = tmp_path / 'w.py'
+    w.write_text(WORKER)
+    rc = bench.spawn(3, [sys.executable, str(w)])
+    out = capfd.readouterr().out
+    assert rc == 0
+    line = json.loads(out.strip().splitlines()[-1])
+    assert line == {'world_size': 3, 'sum': 6.0}
+
+
+def test_spawn_fails_when_a_worker_fails(tmp_path, monkeypatch):
+    w = tmp_path / 'w.py'
+    w.write_text(WORKER)
+    monkeypatch.setenv('FAIL_RANK', '1')
+    assert bench.spawn(2, [sys.executable, str(w)]) == 3
+
+
+def test_spawn_stops_the_others(tmp_path):
+    w = tmp_path / 'w.py'
+    w.write_text('import os, sys, time\nif os.environ["RANK"] == "1": sys.exit(5)\ntime.sleep(600)\n')
+    assert bench.spawn(2, [sys.executable, str(w)]) == 5
+
+
+def test_gpus_must_match_world_size(monkeypatch):
+    monkeypatch.setenv('WORLD_SIZE', '2')
+    args = bench.parse(['--gpus', '4'])
+    with pytest.raises(SystemExit, match='WORLD_SIZE=2'):
+        bench.setup_rank(args)
+
+
+def test_defaults_are_config2():
+    a = bench.parse([])
+    assert (a.config, a.algo, a.clients, a.D, a.C, a.custom) == (2, 'fedavg', 100, 2048, 10, False)
+    assert [c for c, _, _ in bench.LEGS] == [4, 3, 5]
