@@ -19,8 +19,8 @@
  *     exchange part itself; its LAST 256 bytes are an error block whose first
  *     uint32 is set (sticky) when a bounded cross-workgroup wait timed out -- the
  *     caller zeroes the workspace once at allocation, reads that word after the
- *     work and clears it.  Test knob: FS_SPIN_LIMIT=0 in the environment makes
- *     every such launch report a timeout (the error path without a real hang).
+ *     work and clears it.  Test knob: fs_tuning.inject_timeout = 1 makes every
+ *     such launch report a timeout (the error path without a real hang).
  *   - Feature rows are fp32, row-major, with a leading dimension `ld` that is a
  *     multiple of 64 floats (D is zero-padded to ld; padded columns stay exactly 0).
  *   - Return value: 0 on success, negative on error; fs_last_error() returns a
@@ -40,11 +40,56 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 8
+#define FS_ABI_VERSION 9
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
 const char* fs_last_error(void);
+
+/* ------------------------------------------------------------------------- *
+ * Tuning (ABI 9).  Every knob that changes HOW (never what) the kernels compute, as
+ * explicit fields -- the library reads no environment variable.  Process-wide: a launch
+ * reads the values current when it is enqueued.  All-zero = the defaults (what the
+ * planners pick by shape).  fs_set_tuning(NULL) restores them; fs_tuning_size() is for
+ * binding-layout checks.
+ *   mix_solver         0 = by shape, else force one p-solver (FS_SOLVER_*; a forced solver
+ *                      that does not cover the shape falls through to the shape's choice)
+ *   mix_prefetch       L2 prefetch helper workgroups beside the p-solve: 0 = by solver
+ *                      (4 for the quarter-wave solver when Z outgrows the L2s, 16 for qmc),
+ *                      -1 = none, n > 0 = n
+ *   mix_prefetch_lead  steps the helpers run ahead (0 = 16)
+ *   mix_exact_softmax  quarter-wave solvers: 1 = torch's exp(o - m - log sum) form with libm
+ *                      expf / logf (default: e * rcp(sum e) on v_exp_f32 / v_rcp_f32; both
+ *                      within the fp32 tolerance of the reference)
+ *   no_eval_fuse       fs_plan_create: 1 = never carry a deferred evaluation inside a
+ *                      training launch (fs_plan_eval_blocks() is then 0)
+ *   spin_limit         bound of every cross-workgroup spin, in polls (0 = the default)
+ *   inject_timeout     test knob: 1 = every exchanging launch reports a timeout at its first
+ *                      hand-off (the error path without a real hang)
+ * ------------------------------------------------------------------------- */
+#define FS_SOLVER_AUTO 0
+#define FS_SOLVER_REG 1
+#define FS_SOLVER_MC 2
+#define FS_SOLVER_STAGED 3
+#define FS_SOLVER_GLOBAL 4
+#define FS_SOLVER_REG2 5
+#define FS_SOLVER_WAVE 6
+#define FS_SOLVER_QUAD 8
+#define FS_SOLVER_QMC 9
+
+typedef struct fs_tuning {
+  int mix_solver;
+  int mix_prefetch;
+  int mix_prefetch_lead;
+  int mix_exact_softmax;
+  int no_eval_fuse;
+  unsigned spin_limit;
+  int inject_timeout;
+} fs_tuning;
+
+int64_t fs_tuning_size(void);
+int fs_set_tuning(const fs_tuning* t);
+int fs_get_tuning(fs_tuning* t);
 
 /* ------------------------------------------------------------------------- *
  * Host: DataLoader shuffle replay.
@@ -224,9 +269,19 @@ int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, i
  *                       next call's TRAIN launch, on the CUs its client groups
  *                       leave idle (parallel split launches, C <= 16; the same
  *                       per-row arithmetic as fs_eval).  d_eval_hist[2t..] is then
- *                       written by that call; a call without TRAIN, or an AGGREGATE,
- *                       runs the pending evaluation on its own first.  Do not
- *                       defer the last round's evaluation.
+ *                       written by that call.  The pending evaluation reads d_W_g
+ *                       as it is when that next call's launches run: the caller
+ *                       must NOT write d_W_g (its own aggregate, an all-reduce into
+ *                       it, a copy) between the deferring call and the next
+ *                       fs_plan_round.  Which launch carries it: a next call whose
+ *                       phases include TRAIN fuses it into the training launch, which
+ *                       runs before that call's own AGGREGATE rewrites d_W_g; a next
+ *                       call without TRAIN runs it as an fs_eval launch of its own
+ *                       before anything else.  The fp64 sum of the per-block partials
+ *                       then follows the launch's evaluation-block count (CUs left
+ *                       idle), so deferred and standalone losses agree to ~1e-12
+ *                       relative, not bitwise.  Do not defer the last round's
+ *                       evaluation.
  * fs_plan_shuffle(plan, seeds, t) replays round t's N*E training shuffles
  * (DataLoader passes of tools.py:179, client-major / epoch-minor seeds) into slot
  * t % 2 on the plan's side stream -- on the GPU (fs_randperm_device, default) or on

@@ -16,6 +16,9 @@ _c_f32p = C.POINTER(C.c_float)
 _SIGS = {
     'fs_abi_version': (C.c_int, []),
     'fs_last_error': (C.c_char_p, []),
+    'fs_tuning_size': (C.c_int64, []),
+    'fs_set_tuning': (C.c_int, [C.c_void_p]),
+    'fs_get_tuning': (C.c_int, [C.c_void_p]),
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     'fs_libsvm_scan': (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     'fs_libsvm_read': (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
@@ -59,11 +62,19 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
-SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 7: 'rows', 8: 'quad', 9: 'qmc'}
+SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc'}
+SOLVERS = {v: k for k, v in SOLVER_NAMES.items() if k}
+
+
+class Tuning(C.Structure):
+    """fs_tuning (include/fedsim.h), field for field: how -- never what -- the kernels compute."""
+    _fields_ = [('mix_solver', C.c_int), ('mix_prefetch', C.c_int), ('mix_prefetch_lead', C.c_int),
+                ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
+                ('inject_timeout', C.c_int)]
 
 
 class PlanDesc(C.Structure):
@@ -105,11 +116,52 @@ def lib():
             f.argtypes = args
         if h.fs_abi_version() != ABI_VERSION:
             raise FedsimError('libfedsim.so ABI %d != %d' % (h.fs_abi_version(), ABI_VERSION))
+        if h.fs_tuning_size() != C.sizeof(Tuning):
+            raise FedsimError('fs_tuning layout mismatch (%d != %d bytes)' % (h.fs_tuning_size(), C.sizeof(Tuning)))
         if h.fs_plan_desc_size() != C.sizeof(PlanDesc):
             raise FedsimError('fs_plan_desc layout mismatch (%d != %d bytes)' % (h.fs_plan_desc_size(),
                                                                                   C.sizeof(PlanDesc)))
         _lib = h
     return _lib
+
+
+def get_tuning():
+    """The library's current fs_tuning as a dict."""
+    t = Tuning()
+    check(lib().fs_get_tuning(C.byref(t)), 'fs_get_tuning')
+    return {k: getattr(t, k) for k, _ in Tuning._fields_}
+
+
+def set_tuning(**fields):
+    """Set fs_tuning fields (the others keep their current values).  ``mix_solver`` may be a
+    solver name ('quad', 'qmc', ...).  Returns the previous settings (a dict)."""
+    prev = get_tuning()
+    cur = dict(prev)
+    for k, v in fields.items():
+        if k not in cur:
+            raise KeyError('fs_tuning has no field %r' % k)
+        if k == 'mix_solver' and isinstance(v, str):
+            v = 0 if v == 'auto' else SOLVERS[v]
+        cur[k] = int(v)
+    t = Tuning(**cur)
+    check(lib().fs_set_tuning(C.byref(t)), 'fs_set_tuning')
+    return prev
+
+
+class tuning:
+    """Context manager: ``with _lib.tuning(mix_solver='qmc', mix_prefetch=-1): ...`` sets
+    fs_tuning fields for the block and restores the previous values after it."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+
+    def __enter__(self):
+        self.prev = set_tuning(**self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        set_tuning(**self.prev)
+        return False
 
 
 def check(status, what):

@@ -16,6 +16,9 @@ namespace fs {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 
+// ---- the process-wide tuning of fs_set_tuning (host.cpp), read at each launch ----
+fs_tuning tuning();
+
 #define FS_REQUIRE(cond, msg)                                                  \
   do {                                                                         \
     if (!(cond)) return ::fs::fail(FS_EINVAL, std::string(__func__) + ": " + (msg)); \

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -29,9 +30,33 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+static std::mutex g_tune_m;
+static fs_tuning g_tune{};
+
+fs_tuning tuning() {
+  std::lock_guard<std::mutex> lk(g_tune_m);
+  return g_tune;
+}
+
 }  // namespace fs
 
 extern "C" int fs_abi_version(void) { return FS_ABI_VERSION; }
+
+extern "C" int64_t fs_tuning_size(void) { return (int64_t)sizeof(fs_tuning); }
+
+extern "C" int fs_set_tuning(const fs_tuning* t) {
+  if (t && (t->mix_prefetch < -1 || t->mix_prefetch > 224 || t->mix_prefetch_lead < 0))
+    return fs::fail(FS_EINVAL, "fs_set_tuning: mix_prefetch must be in [-1, 224], mix_prefetch_lead >= 0");
+  std::lock_guard<std::mutex> lk(fs::g_tune_m);
+  fs::g_tune = t ? *t : fs_tuning{};
+  return FS_OK;
+}
+
+extern "C" int fs_get_tuning(fs_tuning* t) {
+  if (!t) return fs::fail(FS_EINVAL, "fs_get_tuning: null pointer");
+  *t = fs::tuning();
+  return FS_OK;
+}
 
 extern "C" const char* fs_last_error(void) { return fs::g_last_error.c_str(); }
 

@@ -5,7 +5,8 @@
 // rounded once to float32, exactly as `csr.toarray().astype(np.float32)` rounds it.
 //
 // Format, as load_svmlight_file reads it: one sample per line, `label [qid:q] idx:val ...`,
-// `#` starts a comment, blank / comment-only lines are skipped.  Index base: zero_based = 1
+// `#` starts a comment, blank / comment-only lines are skipped; the indices of a line must
+// be strictly increasing (sorted and unique, else an error, as sklearn's ValueError).  Index base: zero_based = 1
 // (indices start at 0), 0 (start at 1), -1 "auto" (zero-based iff the smallest index in the
 // file is 0 -- sklearn's 'auto').  Width: caller's n_features (scan reports the max index).
 //
@@ -106,6 +107,7 @@ bool walk(Chunk& c, OnRow on_row, OnPair on_pair) {
         while (q < end && *q != ' ' && *q != '\t') ++q;
         q = skip_blank(q, end);
       }
+      long long prev = -1;
       while (q < end) {
         char* s2 = nullptr;
         const long long idx = std::strtoll(q, &s2, 10);
@@ -124,6 +126,12 @@ bool walk(Chunk& c, OnRow on_row, OnPair on_pair) {
           c.err = "line " + std::to_string(line) + ": negative feature index";
           return false;
         }
+        if (idx <= prev) {                           // load_svmlight_file's ValueError
+          c.err = "line " + std::to_string(line) +
+                  ": feature indices in SVMlight/LibSVM data file should be sorted and unique";
+          return false;
+        }
+        prev = idx;
         on_pair((int64_t)idx, val);
         q = skip_blank(s3, end);
       }

@@ -123,30 +123,25 @@ __device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp,
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
 // (fixed q) then reads 64 contiguous bytes of each of 16 rows.
-// NWV: waves per workgroup -- 8 (one workgroup per CU, up to 16 tiles per slice) or 4 (two
-//      workgroups per CU, up to 8 tiles each: two independent client chains share the CU, so
-//      one computes while the other waits on its hand-off or its row loads).
-// SCHED: how the waves share a step's hand-off and the next step's row loads.
-//   0  every wave publishes / polls its share of the values; the first half of the waves
-//      issue their next rows right after the hand-off, the second half after the softmax.
-//   1  the second half writes its image slice and issues its next rows at once (their bytes
-//      stream during the hand-off); the first half alone runs the hand-off (nothing of its
-//      own queued ahead of its polls) and issues its rows after the softmax.
-//   2  every wave runs the hand-off; no wave issues its next rows in a burst: each issues
-//      one row load per backward iteration (16 per wave per step), so the issue stalls of a
-//      full memory queue land between the backward's MFMAs instead of ahead of them.
-// (Tried and dropped, r02q / r02w: the first half interleaving as 2 while the second half
-// streams during the hand-off as 1 -- no faster; 2 plus the first 4 or 8 row loads of each
-// wave issued right after its image write -- slower at every BASELINE shape.)
-template <int RT, int G, bool PROX, int SCHED, int NWV>
-__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_kernel(LTParams P, SplitWS X) {
-  constexpr int NW = NWV;
+// Schedule: every wave runs the hand-off; no wave issues its next rows in a burst: each issues
+// one row load per backward iteration (16 per wave per step), so the issue stalls of a full
+// memory queue land between the backward's MFMAs instead of ahead of them.  Measured and
+// dropped (round 2, r02f / r02q / r02w): two 4-wave workgroups per CU (two client chains per
+// CU); half the waves streaming their next rows during the hand-off while the other half runs
+// it; every wave issuing its rows in a burst after the hand-off or after the softmax; a prefix
+// of 4 or 8 row loads issued right after the image write -- each slower at every BASELINE shape.
+// Round 3: odd groups started half a step late (so half the CUs stream while the other half
+// hand off) changed nothing (configs 2 / 4 / 5 within 0.5 %): the row stream is bound per CU,
+// not by the chip's HBM.
+template <int RT, int G, bool PROX>
+__global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
+  constexpr int NW = SP_WAVES;
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
   constexpr int TPW = SP_TPW;
-  constexpr int XT = SCHED == 1 ? NTH / 2 : NTH;  // threads running the hand-off
+  constexpr int XT = NTH;                         // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
   constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
   constexpr int HC = G;                             // partners polled per round trip
@@ -174,7 +169,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   // idle, LDS from the (unused) image
   const int nb = gridDim.x - P.fuse_E;
   if ((int)blockIdx.x >= nb) {
-    eval_persistent<NWV>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
+    eval_persistent<SP_WAVES>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
                          xs_lds, P.fuse_part);
     return;
   }
@@ -349,13 +344,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
           _Pragma("unroll") for (int q = 0; q < 4; ++q)                              \
             st4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg), xf[i][rt][q]); \
   }
-      // the next step's slice into the (now free) registers, then the row indices after it
-#define SP_NEXT()                                                                    \
-  if (lc_ok) {                                                                       \
-    SP_XLOAD();                                                                      \
-    lc_ok = sp_advance(lc, P, grp, ng, T);                                           \
-    if (lc_ok) fetch_rows();                                                         \
-  }
 
       // ---------------- forward partial: z_g = X_slice W_slice^T ----------------
       floatx4 acc[RT];
@@ -383,11 +371,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
 
-      const bool xw = SCHED != 1 || w < NW / 2;      // this wave runs the hand-off
-      if (!xw) {
-        SP_IMG_WRITE();
-        SP_NEXT();
-      } else {
+      {
         // ---- hand-off, spread over the hand-off threads: thread t owns the values t + XT m
         // (the B x C real logits row-major, then the two norms).  Guideline 16, R2 form:
         // every value travels as one 8-byte {tag, value} granule written by ONE relaxed
@@ -472,7 +456,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
           }
         }
         SP_STAMP(4)
-        if (SCHED == 0 && w < NW / 2) SP_NEXT();
       }
       SP_STAMP(5)
       lds_barrier();  // S2: summed logits and norms, the image
@@ -503,7 +486,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       cep = wave_sum_dpp(cep, lane);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
-      if ((SCHED == 0 && w >= NW / 2) || (SCHED == 1 && w < NW / 2)) SP_NEXT();
       SP_STAMP(7)
       const float pn2 = nrm[0], wn2 = nrm[1];
       if (g == 0 && tid == 0 && e == E - 1) {
@@ -526,8 +508,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
       const float lr = P.lr;
       const int rblk = 4 * (l16 & 3) + (l16 >> 2);
       float npn = 0.f, nwn = 0.f;
-      // schedules 2 / 3: this wave's next rows go out one load per backward iteration
-      const bool ilv = lc_ok && SCHED == 2;
+      // this wave's next rows go out one load per backward iteration
+      const bool ilv = lc_ok;
       // (two instances, so the interleaved loads are straight-line code: a branch around each
       // load would make the compiler wait for it at the join)
       // FULL: every wave owns TPW tiles (NTS = NW * TPW, every BASELINE shape but chained config
@@ -606,7 +588,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void local_train_split_
   }
 #undef SP_XLOAD
 #undef SP_IMG_WRITE
-#undef SP_NEXT
 #ifdef FS_STAMPS
   if (tid == 0 && X.stamps) {
     for (int k = 0; k < 8; ++k) X.stamps[blockIdx.x * 16 + k] = stamp_acc[k];
@@ -638,92 +619,50 @@ static size_t split_static_lds(int RT, int NW) {
 
 static int split_rt(int B) { return B <= 16 ? 1 : 2; }
 
-// waves per workgroup implied by the slice width: 4 (two workgroups per CU) when the slice has
-// at most 8 tiles and two workgroups' LDS fit one CU -- only on request (FS_SPLIT_NW=4): two
-// half-size chains per CU measured slower than one full one at every BASELINE shape (r02f:
-// config 2 462 vs 364 us, config 4 604 vs 497 us, chained config 1 11.4 vs 10.3 ms), since
-// the CU's memory pipe, not the chain's latency, is what both chains wait on
-static int split_nw(int RT, int NT, int G) {
-  const int tiles = (NT + G - 1) / G;
-  const char* force = getenv("FS_SPLIT_NW");
-  if (!(force && atoi(force) == 4)) return 8;
-  if (tiles <= 2 * 4 && 2 * (split_dyn_lds(RT, NT, G) + split_static_lds(RT, 4)) <= 160 * 1024) return 4;
-  return 8;
-}
-
 // can G workgroups split one client of this shape?
 static bool split_fits(int C, int B, int NT, int G) {
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
   if (C > 16 || B > 32 || NT < G) return false;
   const int RT = split_rt(B);
-  const int NW = split_nw(RT, NT, G);
   const int tiles = (NT + G - 1) / G;
-  if ((tiles + NW - 1) / NW > SP_TPW) return false;
+  if ((tiles + SP_WAVES - 1) / SP_WAVES > SP_TPW) return false;
   if (G >= 8 && RT * 16 * C + 2 > 512) return false;   // exchanged values: at most 512
-  return split_dyn_lds(RT, NT, G) + split_static_lds(RT, NW) <= 160 * 1024;
+  return split_dyn_lds(RT, NT, G) + split_static_lds(RT, SP_WAVES) <= 160 * 1024;
 }
 
 static int split_sz(int RT) { return RT * 16 * 16 + 4; }
 
-// groups in flight: one per G workgroups, one workgroup per CU (8 waves) or two (4 waves)
-static int split_groups(int N, int G, int NW, int chained, int cus) {
-  return chained ? 1 : std::max(1, std::min(N, cus * (NW == 4 ? 2 : 1) / G));
+// groups in flight: one per G workgroups, one workgroup per CU
+static int split_groups(int N, int G, int chained, int cus) {
+  return chained ? 1 : std::max(1, std::min(N, cus / G));
 }
 
 static int64_t split_xbuf_bytes(int ngroups, int G, int RT) { return (int64_t)ngroups * 2 * G * split_sz(RT) * 8; }
 
-static int64_t split_ws_bytes(int N, int G, int B, int NT, int chained, int cus) {
+static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus) {
   const int RT = split_rt(B);
-  return split_xbuf_bytes(split_groups(N, G, split_nw(RT, NT, G), chained, cus), G, RT) + SP_ERR_BYTES;
+  return split_xbuf_bytes(split_groups(N, G, chained, cus), G, RT) + SP_ERR_BYTES;
 }
 
+// the hand-off spin bound (fs_tuning.spin_limit); 0 = the injected-timeout test knob
 static unsigned split_spin_limit() {
-  const char* s = getenv("FS_SPIN_LIMIT");        // test knob: 0 injects a hand-off timeout
-  return s ? (unsigned)strtoul(s, nullptr, 10) : SP_SPIN_LIMIT;
-}
-
-template <int RT, int G, bool PROX, int SCHED, int NW>
-static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, SCHED, NW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, SCHED, NW>), dim3(grid), dim3(NW * 64), lds, st, P, X);
-}
-
-// default: 2 for 8-wave workgroups -- r02q, us per launch, schedules 0 / 1 / 2: config 2
-// (G = 2) 365 / 367 / 353; config 4 (G = 2) 513 / 503 / 483; config 3 (G = 4) 5085 / 5169 /
-// 4860; config 5 (G = 16) 6692 / - / 6187; chained config 1 (G = 8) 9066 / 9576 / 8456.
-// 4-wave workgroups (opt-in) keep 0.
-static int split_sched(int G, int NW, bool chained) {
-  (void)G;
-  (void)chained;
-  const char* s = getenv("FS_SP_SCHED");          // diagnostics: force a schedule variant
-  if (s) return std::max(0, std::min(2, atoi(s)));
-  return NW == 4 ? 0 : 2;
+  const fs_tuning t = tuning();
+  if (t.inject_timeout) return 0u;
+  return t.spin_limit ? t.spin_limit : SP_SPIN_LIMIT;
 }
 
 template <int RT, int G, bool PROX>
-static void launch_split_p(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
-  const int sc = split_sched(G, NW, P.chained != 0);
-  if (NW == 8 && sc == 2) {
-    launch_split_s<RT, G, PROX, 2, 8>(P, X, grid, lds, st);
-  } else if constexpr (G >= 16) {
-    launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);     // the hand-off values need all 512 threads
-  } else {
-    if (NW == 4) {
-      if (sc == 0) launch_split_s<RT, G, PROX, 0, 4>(P, X, grid, lds, st);
-      else launch_split_s<RT, G, PROX, 1, 4>(P, X, grid, lds, st);
-    } else {
-      if (sc == 0) launch_split_s<RT, G, PROX, 0, 8>(P, X, grid, lds, st);
-      else launch_split_s<RT, G, PROX, 1, 8>(P, X, grid, lds, st);
-    }
-  }
+static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
 }
 
 template <int RT, int G>
-static void launch_split_g(const LTParams& P, const SplitWS& X, int NW, int grid, size_t lds, hipStream_t st) {
-  if (P.prox) launch_split_p<RT, G, true>(P, X, NW, grid, lds, st);
-  else launch_split_p<RT, G, false>(P, X, NW, grid, lds, st);
+static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if (P.prox) launch_split_s<RT, G, true>(P, X, grid, lds, st);
+  else launch_split_s<RT, G, false>(P, X, grid, lds, st);
 }
 
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
@@ -736,8 +675,7 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
   if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");
-  const int NW = split_nw(RT, NT, G);
-  const int ng = split_groups(P.N, G, NW, P.chained, cus);
+  const int ng = split_groups(P.N, G, P.chained, cus);
   const int64_t xbytes = split_xbuf_bytes(ng, G, RT);
   if (!ws || ws_bytes < xbytes + SP_ERR_BYTES) return fail(FS_EINVAL, "fs_local_train: workspace too small");
   char* base = reinterpret_cast<char*>(ws);
@@ -776,11 +714,11 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
     if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
   }
   const size_t lds = split_dyn_lds(RT, NT, G);
-  if (P.fuse_E > 0 && (P.chained || NW != 8 || ng * G + P.fuse_E > cus || lds < sizeof(float) * NW * 16 * 17))
+  if (P.fuse_E > 0 && (P.chained || ng * G + P.fuse_E > cus || lds < sizeof(float) * SP_WAVES * 16 * 17))
     return fail(FS_EINVAL, "fs_local_train: no room for the fused evaluation");
   const int grid = P.chained ? 8 * G : ng * G + P.fuse_E;
 #define FS_SPLIT_CASE(rt, g) \
-  if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, NW, grid, lds, st); return FS_OK; }
+  if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, grid, lds, st); return FS_OK; }
   FS_SPLIT_CASE(2, 2) FS_SPLIT_CASE(2, 4) FS_SPLIT_CASE(2, 8) FS_SPLIT_CASE(2, 16)
   FS_SPLIT_CASE(1, 2) FS_SPLIT_CASE(1, 4) FS_SPLIT_CASE(1, 8) FS_SPLIT_CASE(1, 16)
 #undef FS_SPLIT_CASE
@@ -791,10 +729,8 @@ int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained) {
   const int NT = (int)(ld >> 6);
   if (chained || G < 2 || C > 16 || B > 32 || !split_fits(C, B, NT, G)) return 0;
   const int cus = device_cus();
-  const int RT = split_rt(B);
-  const int NW = split_nw(RT, NT, G);
-  if (cus <= 0 || NW != 8) return 0;
-  return std::max(0, cus - split_groups(N, G, NW, 0, cus) * G);
+  if (cus <= 0) return 0;
+  return std::max(0, cus - split_groups(N, G, 0, cus) * G);
 }
 
 }  // namespace fs
@@ -805,18 +741,16 @@ using namespace fs;
 // a group of G workgroups splits the feature dimension of one client at a time) and the
 // workspace bytes it needs.  On entry *G_out is a request: 0 = let the planner choose,
 // 1 = one workgroup per client, 2..16 = that group width if the shape allows it (else the
-// planner's choice).  FS_SPLIT_G in the environment overrides a 0 request (diagnostics).
+// planner's choice).
 // prox: the FedProx term is on (kept in the ABI; every split variant covers it).
 // max_en = max_j E * n_j.
 extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                                    int* G_out, int64_t* ws_bytes_out) {
   FS_REQUIRE(G_out && ws_bytes_out, "null pointer");
   FS_REQUIRE(N >= 1 && B >= 1 && ld >= 64 && ld % 64 == 0, "bad sizes");
-  int want = *G_out;
+  const int want = *G_out;
   *G_out = 1;
   *ws_bytes_out = 0;
-  if (want == 0)
-    if (const char* s = getenv("FS_SPLIT_G")) want = atoi(s);
   const int cus = device_cus();
   if (want == 1 || C > 16 || B > 32 || cus <= 0) return FS_OK;
   const int NT = (int)(ld >> 6);
@@ -844,6 +778,6 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   (void)E;
   if (G == 0) return FS_OK;
   *G_out = G;
-  *ws_bytes_out = split_ws_bytes(N, G, B, NT, chained, cus);
+  *ws_bytes_out = split_ws_bytes(N, G, B, chained, cus);
   return FS_OK;
 }

@@ -635,295 +635,6 @@ static bool mix_solve_reg(hipStream_t st, const float* Z, const int32_t* y, cons
 }
 
 // ----------------------------------------------------------------------------
-// p-solve, row-split form (Bv <= 16, N <= 64*NK, C <= CL): the register solver's layout on
-// K = 16/RW workgroups, workgroup k owning batch rows k*RW .. k*RW+RW-1 of every step.  A
-// workgroup has its rows' full Z rows, so it computes their logits, softmax and CE gradient
-// alone; the one cross-CU exchange of a step is the partial gradient of p (N values):
-// wave 0 publishes its workgroup's sum (8-byte {tag, value} granules, as the multi-CU
-// solver), reads the K partials back and folds them in workgroup order -- the same bits in
-// every workgroup, so every copy of p and of the momentum buffer stays identical.  Per step a
-// CU gathers 16*C*N*4 / K bytes of Z instead of all of it (one CU gathering random rows is the
-// register solver's bound, section 4.5 of DESIGN.md), for one hop of N values.
-// 8*K blocks are launched and those with blockIdx % 8 == 0 take part (one XCD under
-// round-robin placement; speed only).  Spins are bounded; a timeout sets the error word
-// and poisons p with NaN.
-// Measured (r02ae/af): no faster than the register solver at config 2 (2.40 vs 2.45 us per
-// step at K = 4; 3.0 at K = 8, 4.4 at K = 16) -- the hop costs what the split gather saves
-// (DESIGN.md section 4.5), so it runs only when forced (FS_MIX_SOLVER=rows).
-// ----------------------------------------------------------------------------
-// Row-split solver's exchange: publish this workgroup's partial gradient (NK values per lane,
-// lanes' clients n0 + j) under `tag`, read the K partials -- all granules issued at once, the
-// missing ones re-read -- and fold them in workgroup order into tot.
-template <int NK, int KMAX>
-__device__ __forceinline__ void mrr_exchange(unsigned long long* slot, int k, int K, int n0, unsigned tag,
-                                             const float (&gk)[NK], float (&tot)[NK], bool& dead,
-                                             unsigned spin_limit, unsigned* err) {
-  constexpr int SLOT = NK * 64;
-#pragma unroll
-  for (int j = 0; j < NK; ++j)
-    __hip_atomic_store(slot + (int64_t)k * SLOT + n0 + j,
-                       ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(gk[j]),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned long long gr[KMAX][NK];
-  unsigned spins = 0;
-  for (;;) {
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q)
-#pragma unroll
-      for (int j = 0; j < NK; ++j)
-        if (q < K && q != k)
-          gr[q][j] = __hip_atomic_load(slot + (int64_t)q * SLOT + n0 + j, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    bool ok = true;
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q)
-#pragma unroll
-      for (int j = 0; j < NK; ++j)
-        if (q < K && q != k) ok = ok && (unsigned)(gr[q][j] >> 32) == tag;
-    if (ok || dead) break;
-    if (++spins > spin_limit) {
-      dead = true;
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NK; ++j) {
-    float a = 0.f;
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q)
-      if (q < K) a += q == k ? gk[j] : __uint_as_float((unsigned)gr[q][j]);
-    tot[j] = a;
-  }
-}
-
-template <int NK, int CP, int CL, int RW, int DEPTH>
-__global__ __launch_bounds__(RW * 64) void mix_solve_rows_kernel(const float* __restrict__ Z,
-                                                                const int32_t* __restrict__ y,
-                                                                const int32_t* __restrict__ perms, int N, int C,
-                                                                int nv, int epochs, int Bv, float lr, float mom,
-                                                                float* __restrict__ p, float* __restrict__ buf,
-                                                                int* __restrict__ first_flag,
-                                                                unsigned long long* __restrict__ xbuf,
-                                                                unsigned* __restrict__ err, int K,
-                                                                unsigned spin_limit) {
-  static_assert(CL <= CP && CP <= 32 && (CP & (CP - 1)) == 0, "class padding");
-  static_assert(DEPTH * (CL + 2) <= 63, "ring vs the vmcnt window");
-  if (blockIdx.x % 8) return;
-  typedef typename MRVec<NK>::T vec;
-  constexpr int LPC = 64 / CP;
-  constexpr int SLOT = NK * 64;                     // granules per workgroup and parity
-  constexpr int KMAX = 16 / RW;
-  __shared__ __attribute__((aligned(16))) float gpart[RW > 1 ? 2 : 1][RW][NK * 64];
-  __shared__ __attribute__((aligned(16))) float gtot[RW > 1 ? 2 : 1][NK * 64];
-  const int k = blockIdx.x / 8;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int row = k * RW + w;                       // this wave's batch row
-  const int ldN = mix_ldn(N);
-  const int CN = C * ldN;
-  const int nbat = (nv + Bv - 1) / Bv;
-  const int total = epochs * nbat;
-  const int n0 = NK * lane;
-  float pr[NK], br[NK];
-#pragma unroll
-  for (int j = 0; j < NK; ++j) {
-    const int n = n0 + j;
-    pr[j] = n < N ? p[n] : 0.f;
-    br[j] = n < N ? buf[n] : 0.f;
-  }
-  int first = *first_flag;
-  const float invB = 1.0f / (float)Bv;
-  const uint32_t nbyte = 4u * (uint32_t)min(n0, ldN - NK);
-  bool dead = false;
-  if (spin_limit == 0 && k == 0 && tid == 0 && total > 0)   // test knob: report an injected timeout
-    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  vec zr[DEPTH][CL];
-  int lab[DEPTH], idxr[DEPTH];
-  auto row_of = [&](int st) -> int {               // perms entry of lane `lane` (a batch row) in step st
-    const int ep = st / nbat, sb = st - ep * nbat;
-    const int b = sb * Bv + lane;
-    const int64_t at = (lane < Bv && b < nv && st < total) ? (int64_t)ep * nv + b : 0;
-    return perms[at];
-  };
-#define MRR_ISSUE(R_, IDXV_)                                                               \
-  {                                                                                        \
-    const int vrow_ = __builtin_amdgcn_readlane((IDXV_), row < 16 ? row : 0);              \
-    const char* zp_ = reinterpret_cast<const char*>(Z + (int64_t)vrow_ * CN);              \
-    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                       \
-      const char* zc_ = zp_ + 4 * (int64_t)(min(c, C - 1) * ldN);                          \
-      zr[R_][c] = *reinterpret_cast<const vec*>(__builtin_assume_aligned(zc_ + nbyte, 4 * NK)); \
-    }                                                                                      \
-    lab[R_] = y[(IDXV_)];                                                                  \
-  }
-  {
-#pragma unroll
-    for (int r0 = 0; r0 < DEPTH; ++r0) {
-      const int iv = row_of(r0);
-      MRR_ISSUE(r0, iv);
-    }
-#pragma unroll
-    for (int r0 = 0; r0 < DEPTH; ++r0) idxr[r0] = row_of(DEPTH + r0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): the loop inherits only its own order
-  }
-  int s = 0;
-#define MRR_STEP(R_)                                                                       \
-  {                                                                                        \
-    if (s >= total) break;                                                                 \
-    const int idx_cur = idxr[R_];                                                          \
-    idxr[R_] = row_of(s + 2 * DEPTH);                                                      \
-    const int bc = min(Bv, nv - (s % nbat) * Bv);                                          \
-    float gme[NK];                                                                         \
-    _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] = 0.f;                           \
-    if (row < bc) {                                                                        \
-      float v[CP];                                                                         \
-      _Pragma("unroll") for (int c = 0; c < CP; ++c) {                                     \
-        float a = 0.f;                                                                     \
-        if (c < CL) {                                                                      \
-          _Pragma("unroll") for (int j = 0; j < NK; ++j) a += mr_el<NK>(zr[R_][c], j) * pr[j]; \
-        }                                                                                  \
-        v[c] = a;                                                                          \
-      }                                                                                    \
-      const float o = class_totals<CP>(v, lane);                                           \
-      const int cls = lane / LPC;                                                          \
-      const bool real = cls < C;                                                           \
-      const float m = class_max<LPC>(real ? o : -INFINITY, lane);                          \
-      const float e = class_sum<LPC>(real ? expf(o - m) : 0.f, lane);                      \
-      const float lse = logf(e);                                                           \
-      const float invb = bc == Bv ? invB : 1.0f / (float)bc;                               \
-      const int yy = __builtin_amdgcn_readlane(lab[R_], row);                              \
-      const float g = (cls == yy ? -invb : 0.f) + expf(o - m - lse) * invb;                \
-      _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                     \
-        if (c < C) {                                                                       \
-          const float gc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(            \
-              __builtin_bit_cast(int, g), c * LPC));                                       \
-          _Pragma("unroll") for (int j = 0; j < NK; ++j) gme[j] += gc * mr_el<NK>(zr[R_][c], j); \
-        }                                                                                  \
-      }                                                                                    \
-    }                                                                                      \
-    const int par = s & 1;                                                                 \
-    float tot[NK];                                                                         \
-    if constexpr (RW > 1) {                                                                \
-      _Pragma("unroll") for (int j = 0; j < NK; ++j) gpart[par][w][n0 + j] = gme[j];       \
-      lds_barrier();                                                                       \
-    }                                                                                      \
-    if (RW == 1 || w == 0) {                                                               \
-      float gk[NK];                                                                        \
-      _Pragma("unroll") for (int j = 0; j < NK; ++j) {                                     \
-        float a = gme[j];                                                                  \
-        if constexpr (RW > 1) {                                                            \
-          a = 0.f;                                                                         \
-          _Pragma("unroll") for (int i = 0; i < RW; ++i) a += gpart[par][i][n0 + j];       \
-        }                                                                                  \
-        gk[j] = a;                                                                         \
-      }                                                                                    \
-      mrr_exchange<NK, KMAX>(xbuf + (int64_t)par * K * SLOT, k, K, n0, (unsigned)s + 1u, gk, tot, \
-                             dead, spin_limit, err);                                       \
-      if constexpr (RW > 1) {                                                              \
-        _Pragma("unroll") for (int j = 0; j < NK; ++j) gtot[par][n0 + j] = tot[j];         \
-      }                                                                                    \
-    }                                                                                      \
-    if constexpr (RW > 1) {                                                                \
-      lds_barrier();                                                                       \
-      _Pragma("unroll") for (int j = 0; j < NK; ++j) tot[j] = gtot[par][n0 + j];           \
-    }                                                                                      \
-    _Pragma("unroll") for (int j = 0; j < NK; ++j)                                         \
-      if (n0 + j < N) momentum_step(pr[j], br[j], tot[j], first, mom, lr);                 \
-    first = 0;                                                                             \
-    /* the ring slot refills only now: the exchange's polls would wait behind it (refilling \
-       before the exchange measured the same, r02af) */                                    \
-    MRR_ISSUE(R_, idx_cur);                                                                \
-    ++s;                                                                                   \
-  }
-  for (;;) {
-    MRR_STEP(0)
-    if constexpr (DEPTH > 1) MRR_STEP(1)
-    if constexpr (DEPTH > 2) MRR_STEP(2)
-  }
-#undef MRR_STEP
-#undef MRR_ISSUE
-  if (k == 0 && w == 0) {
-#pragma unroll
-    for (int j = 0; j < NK; ++j) {
-      const int n = n0 + j;
-      if (n < N) {
-        p[n] = dead ? __int_as_float(0x7fc00000) : pr[j];
-        buf[n] = br[j];
-      }
-    }
-    if (lane == 0 && total > 0) *first_flag = 0;
-  }
-}
-
-// exchange granules of the row-split solver: [2][K][64*NK], zeroed before every launch
-static int64_t mrr_xbytes(int N) {
-  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : 4);
-  return (int64_t)sizeof(unsigned long long) * 2 * 16 * 64 * nk;
-}
-
-static bool mrr_covers(int N, int C, int Bv) { return Bv <= 16 && N <= 256 && C <= 16; }
-
-// rows per workgroup: FS_MIX_ROWS_RW=1|2|4|8 (diagnostics), default 4 -- r02ae/af, N = 100,
-// C = 10, us per step, RW = 1 / 2 / 4 / 8 (K = 16 / 8 / 4 / 2): 4.41 / 3.00 / 2.40 / 2.46
-// (the register solver: 2.45)
-static int mrr_rw() {
-  const char* env = getenv("FS_MIX_ROWS_RW");
-  const int r = env ? atoi(env) : 4;
-  return (r == 1 || r == 2 || r == 8) ? r : 4;
-}
-
-template <int NK, int CP, int CL, int RW>
-static void launch_mix_rows(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
-                            int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
-                            unsigned long long* xbuf, unsigned* err, unsigned spin_limit) {
-  constexpr int depth = 3 * (CL + 2) <= 63 ? 3 : 2;
-  const int K = (Bv + RW - 1) / RW;
-  hipLaunchKernelGGL((mix_solve_rows_kernel<NK, CP, CL, RW, depth>), dim3(8 * K), dim3(RW * 64), 0, st, Z, y,
-                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, xbuf, err, K, spin_limit);
-}
-
-static unsigned mc_spin_limit();
-
-// row-split solver for (N, C, Bv) if an instance covers it: 1 launched, 0 not covered, < 0 error
-static int mix_solve_rows(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
-                          int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
-                          void* d_ws, int64_t ws_bytes, int64_t err_bytes) {
-  if (!mrr_covers(N, C, Bv)) return 0;
-  const int64_t xbytes = mrr_xbytes(N);
-  if (!d_ws || ws_bytes < xbytes + err_bytes)
-    return fail(FS_EINVAL, "fs_mix_solve: workspace too small (see fs_mix_solve_ws_bytes)");
-  unsigned long long* ws = reinterpret_cast<unsigned long long*>(d_ws);
-  unsigned* err = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - err_bytes);
-  const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : 4);
-  const int rw = mrr_rw();
-  const unsigned spin_limit = mc_spin_limit();
-  bool launched = false;
-#define MRR_CASE(NK_, CP_, CL_)                                                                            \
-  if (!launched && nk == NK_ && C <= CL_) {                                                                \
-    hipError_t e = hipMemsetAsync(ws, 0, (size_t)xbytes, st);                                              \
-    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));      \
-    if (rw == 1)                                                                                           \
-      launch_mix_rows<NK_, CP_, CL_, 1>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
-                                        spin_limit);                                                       \
-    else if (rw == 2)                                                                                      \
-      launch_mix_rows<NK_, CP_, CL_, 2>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
-                                        spin_limit);                                                       \
-    else if (rw == 8)                                                                                      \
-      launch_mix_rows<NK_, CP_, CL_, 8>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
-                                        spin_limit);                                                       \
-    else                                                                                                   \
-      launch_mix_rows<NK_, CP_, CL_, 4>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, ws, err, \
-                                        spin_limit);                                                       \
-    launched = true;                                                                                       \
-  }
-  MRR_CASE(1, 2, 2) MRR_CASE(1, 4, 4) MRR_CASE(1, 8, 8) MRR_CASE(1, 16, 10) MRR_CASE(1, 16, 16)
-  MRR_CASE(2, 2, 2) MRR_CASE(2, 4, 4) MRR_CASE(2, 8, 8) MRR_CASE(2, 16, 10) MRR_CASE(2, 16, 16)
-  MRR_CASE(4, 2, 2) MRR_CASE(4, 4, 4) MRR_CASE(4, 8, 8) MRR_CASE(4, 16, 10)
-#undef MRR_CASE
-  return launched ? 1 : 0;
-}
-
-// ----------------------------------------------------------------------------
 // p-solve, register-resident form 2 (Bv <= 16, C <= CL <= 10, N <= 64*NK): the register
 // solver above is VALU-bound (rocprofv3: the SIMDs' vector pipes ~80 % busy at config 2);
 // this form does the same arithmetic in fewer vector instructions per step:
@@ -941,15 +652,15 @@ static int mix_solve_rows(hipStream_t st, const float* Z, const int32_t* y, cons
 constexpr int M2_WAVES = 8;
 
 // class_totals of lanes.h for two independent rows at once (the levels interleave)
-template <int CP, bool SWAP>
+template <int CP>
 __device__ __forceinline__ void class_totals2(float (&v0)[CP], float (&v1)[CP], int lane, float& o0, float& o1) {
   constexpr int LPC = 64 / CP;
 #define M2_LEVEL(OFF_)                                                              \
   if constexpr (CP >= 64 / (OFF_)) {                                               \
     constexpr int L_ = CP / (32 / (OFF_));                                         \
     _Pragma("unroll") for (int i = 0; i < L_ / 2; ++i) {                           \
-      v0[i] = rs_level<OFF_, SWAP>(v0[i], v0[i + L_ / 2], lane);                   \
-      v1[i] = rs_level<OFF_, SWAP>(v1[i], v1[i + L_ / 2], lane);                   \
+      v0[i] = rs_level<OFF_, true>(v0[i], v0[i + L_ / 2], lane);                   \
+      v1[i] = rs_level<OFF_, true>(v1[i], v1[i + L_ / 2], lane);                   \
     }                                                                              \
   }
   M2_LEVEL(32) M2_LEVEL(16) M2_LEVEL(8) M2_LEVEL(4) M2_LEVEL(2) M2_LEVEL(1)
@@ -964,7 +675,7 @@ __device__ __forceinline__ void class_totals2(float (&v0)[CP], float (&v1)[CP], 
   o1 = b;
 }
 
-template <int NK, int CP, int CL, int DEPTH, bool SWAP>
+template <int NK, int CP, int CL, int DEPTH>
 __global__ __launch_bounds__(M2_WAVES * 64) void mix_solve_reg2_kernel(const float* __restrict__ Z,
                                                                       const int32_t* __restrict__ y,
                                                                       const int32_t* __restrict__ perms, int N, int C,
@@ -1067,7 +778,7 @@ __global__ __launch_bounds__(M2_WAVES * 64) void mix_solve_reg2_kernel(const flo
       v1[c] = b;                                                                           \
     }                                                                                      \
     float o0, o1;                                                                          \
-    class_totals2<CP, SWAP>(v0, v1, lane, o0, o1);                                         \
+    class_totals2<CP>(v0, v1, lane, o0, o1);                                         \
     const int cls = lane / LPC;                                                            \
     const bool real = cls < C;                                                             \
     const float m0 = class_max<LPC>(real ? o0 : -INFINITY, lane);                          \
@@ -1129,14 +840,10 @@ __global__ __launch_bounds__(M2_WAVES * 64) void mix_solve_reg2_kernel(const flo
 template <int NK, int CP, int CL>
 static void launch_mix_reg2(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
                             int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
-                            int z_bytes, bool swap) {
+                            int z_bytes) {
   constexpr int depth = 2 * CL * 3 <= 63 ? 3 : (2 * CL * 2 <= 63 ? 2 : 1);
-  if (swap)
-    hipLaunchKernelGGL((mix_solve_reg2_kernel<NK, CP, CL, depth, true>), dim3(1), dim3(M2_WAVES * 64), 0, st, Z, y,
-                       perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes);
-  else
-    hipLaunchKernelGGL((mix_solve_reg2_kernel<NK, CP, CL, depth, false>), dim3(1), dim3(M2_WAVES * 64), 0, st, Z, y,
-                       perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes);
+  hipLaunchKernelGGL((mix_solve_reg2_kernel<NK, CP, CL, depth>), dim3(1), dim3(M2_WAVES * 64), 0, st, Z, y,
+                     perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes);
 }
 
 // register-resident solver, form 2, for (N, C, Bv) if an instance covers it
@@ -1145,12 +852,10 @@ static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, con
   if (Bv > 2 * M2_WAVES || C > 10) return false;
   const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
   if (zb >= ((int64_t)1 << 31) || (int64_t)epochs * nv >= ((int64_t)1 << 31)) return false;   // 32-bit offsets
-  const char* sw = getenv("FS_MIX_SWAP");        // diagnostics: 0 = select-form reduce-scatter
-  const bool swap = !(sw && atoi(sw) == 0);
   const int nk = N <= 64 ? 1 : (N <= 128 ? 2 : (N <= 256 ? 4 : 0));
 #define M2_CASE(NK_, CP_, CL_)                                                                              \
   if (nk == NK_ && C <= CL_) {                                                                              \
-    launch_mix_reg2<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, (int)zb, swap); \
+    launch_mix_reg2<NK_, CP_, CL_>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, (int)zb);       \
     return true;                                                                                            \
   }
   M2_CASE(1, 2, 2) M2_CASE(1, 4, 4) M2_CASE(1, 8, 8) M2_CASE(1, 16, 10)
@@ -1197,7 +902,7 @@ template <int NK, int CL, int DEPTH, int SPL, bool FASTX>
 __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
     int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
-    int* __restrict__ first_flag, int z_bytes, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead, int oob) {
+    int* __restrict__ first_flag, int z_bytes, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead) {
   static_assert(NK == 4 || NK == 8, "clients per lane");
   static_assert(CL >= 1 && CL <= 16, "classes");
   static_assert(DEPTH * (CL * NK / 4 + 2) <= 63, "ring vs the vmcnt window");
@@ -1238,11 +943,10 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
   int first = *first_flag;
   // lane byte offsets of its client chunks inside a class segment; a chunk wholly past ldN
   // gets an offset beyond the buffer's range: the load returns zeros without a memory access
-  // (FS_MIX_QUAD_OOB=0: such chunks re-read the last real one instead -- their p is 0 either way)
   uint32_t lofs[NV4];
 #pragma unroll
   for (int h = 0; h < NV4; ++h)
-    lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : (oob ? 0x80000000u : 4u * (uint32_t)(ldN - 4));
+    lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : 0x80000000u;
   int sofs[CL];
 #pragma unroll
   for (int c = 0; c < CL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * ldN);
@@ -1394,11 +1098,6 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
   }
 }
 
-static int quad_oob() {
-  const char* e = getenv("FS_MIX_QUAD_OOB");
-  return e && atoi(e) == 0 ? 0 : 1;
-}
-
 // default issue split: about 3/10 of the classes at the end of a step, the rest after the next
 // step's logits (r02s2j/k, config 2: 1.65 us per step unsplit, 1.42-1.47 split 3 or 5 without
 // helpers, 1.35-1.43 with 4 helpers; split 3 also keeps the (8, 10) instance in 242 VGPRs)
@@ -1414,16 +1113,15 @@ static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, co
   const int blocks = pf.prog ? 8 * std::min(pf.h, 31) + 1 : 1;   // helpers: the solver's XCD only
   // softmax on v_exp_f32 / v_rcp_f32 (e / sum) by default: config 2 1.28-1.29 -> 1.21-1.23 us per
   // step (r02s2fx), within the fp32 tolerance of the oracle like every other solver;
-  // FS_MIX_QUAD_FASTEXP=0: torch's exp(o - m - log(sum)) form with libm expf / logf
-  const char* fx = getenv("FS_MIX_QUAD_FASTEXP");
-  if (!(fx && atoi(fx) == 0))
+  // fs_tuning.mix_exact_softmax: torch's exp(o - m - log(sum)) form with libm expf / logf
+  if (!tuning().mix_exact_softmax)
     hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL, true>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z,
                        y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
-                       pf.lead, quad_oob());
+                       pf.lead);
   else
     hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL, false>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z,
                        y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
-                       pf.lead, quad_oob());
+                       pf.lead);
 }
 
 static bool quad_covers(int N, int C, int Bv, int nv, int epochs) {
@@ -1443,18 +1141,7 @@ static bool mix_solve_quad(hipStream_t st, const float* Z, const int32_t* y, con
     return true;                                                                                             \
   }
   MQ_CASE(4, 2) MQ_CASE(4, 4) MQ_CASE(4, 8) MQ_CASE(4, 10) MQ_CASE(4, 16)
-  MQ_CASE(8, 2) MQ_CASE(8, 4) MQ_CASE(8, 8)
-  if (nk == 8 && C <= 10) {
-    // issue split (diagnostics, FS_MIX_QUAD_SPLIT): classes issued at the end of a step; the
-    // rest go out in the next step after its logits
-    const char* e = getenv("FS_MIX_QUAD_SPLIT");
-    const int spl = e ? atoi(e) : 3;
-    if (spl == 10) launch_mix_quad<8, 10, 10>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
-    else if (spl == 5) launch_mix_quad<8, 10, 5>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
-    else if (spl == 7) launch_mix_quad<8, 10, 7>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
-    else launch_mix_quad<8, 10>(st, Z, y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, zb, pf);
-    return true;
-  }
+  MQ_CASE(8, 2) MQ_CASE(8, 4) MQ_CASE(8, 8) MQ_CASE(8, 10)
 #undef MQ_CASE
   return false;
 }
@@ -1634,7 +1321,7 @@ __device__ __forceinline__ bool mc_wait(const unsigned long long* g, unsigned ta
 // the exchange waits, but every poll queues behind it: a hop between streaming CUs costs ~3x
 // an idle one, MI355X_MICROARCH.md handoff-1to1), 1 after hop 1 (HOPS = 2: hop 1 runs with
 // an empty queue), 2 after the exchange (both hops idle, the slice's latency exposed).
-template <int S, int HOPS, int ZAT>
+template <int S, int HOPS>
 __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* __restrict__ Z,
                                                                  const int32_t* __restrict__ y,
                                                                  const int32_t* __restrict__ perms, int N, int C,
@@ -1710,7 +1397,6 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
       for (int i = 0; i < S / 4; ++i) zn[i] = ld4(zr + coff[i]);
       yn = y[vnext];
     };
-    if constexpr (ZAT == 0 || (ZAT == 1 && HOPS == 1)) issue_next();
     const int vn2 = row_at(st + 2);
     // ---- partial logits of this workgroup's clients ----
     float a = 0.f;
@@ -1772,7 +1458,6 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
           part[u] = __uint_as_float((unsigned)gv);
         }
       }
-      if constexpr (ZAT == 1) issue_next();
       lds_barrier();
       if (t < nown) {                              // fold in workgroup order, publish the total
         float sum = 0.f;
@@ -1788,7 +1473,7 @@ __global__ __launch_bounds__(MC_THREADS) void mix_solve_mc_kernel(const float* _
         o = __uint_as_float((unsigned)gv);
       }
     }
-    if constexpr (ZAT == 2) issue_next();
+    issue_next();
     // ---- softmax-CE gradient of row b (16-lane class groups) ----
     const int sb = st % nbat;
     const int bc = min(Bv, nv - sb * Bv);
@@ -1840,28 +1525,22 @@ constexpr int64_t MC_ERR_BYTES = 256;
 
 static int64_t mc_xbytes(int K) { return (int64_t)sizeof(unsigned long long) * 2 * (K * MC_SLOT + MC_TOT); }
 
-// exchange form: FS_MIX_MC_HOPS=1|2 (diagnostics).  Default two hops, except at S = 8 -- r02n,
-// N = 100, C = 10, us per step, one hop / two hops (Z issued after the exchange): S = 64 (K = 2)
-// 5.50 / 4.14, S = 32 (K = 4) 4.43 / 2.90, S = 16 (K = 7) 3.95 / 2.87, S = 8 (K = 13) 3.25 / 3.79
-static int mc_hops(int K, int S) {
-  const char* env = getenv("FS_MIX_MC_HOPS");
-  if (env && (atoi(env) == 1 || atoi(env) == 2)) return atoi(env);
-  return (K >= 2 && S >= 16) ? 2 : 1;
-}
+// exchange form: two hops, except at S = 8 (one) -- r02n, N = 100, C = 10, us per step, one hop /
+// two hops (Z issued after the exchange): S = 64 (K = 2) 5.50 / 4.14, S = 32 (K = 4) 4.43 / 2.90,
+// S = 16 (K = 7) 3.95 / 2.87, S = 8 (K = 13) 3.25 / 3.79
+static int mc_hops(int K, int S) { return (K >= 2 && S >= 16) ? 2 : 1; }
 
+// the exchange kernels' spin bound (fs_tuning.spin_limit) and the injected-timeout test knob
+// (the kernels report a timeout at the first exchange when the bound they get is 0)
 static unsigned mc_spin_limit() {
-  const char* s = getenv("FS_SPIN_LIMIT");        // test knob: 0 injects an exchange timeout
-  return s ? (unsigned)strtoul(s, nullptr, 10) : MC_SPIN_LIMIT;
+  const fs_tuning t = tuning();
+  if (t.inject_timeout) return 0u;
+  return t.spin_limit ? t.spin_limit : MC_SPIN_LIMIT;
 }
 
 // slice width for N clients (0: not covered): S clients per workgroup, K = ceil(ldN / S) <= 32
 static int mc_slice(int N) {
   const int ldN = mix_ldn(N);
-  const char* env = getenv("FS_MIX_MC_S");
-  if (env) {
-    const int s = atoi(env);
-    if ((s == 8 || s == 16 || s == 32 || s == 64) && (ldN + s - 1) / s <= MC_KMAX) return s;
-  }
   for (int s : {8, 16, 32, 64})
     if ((ldN + s - 1) / s <= MC_KMAX && (s > 8 || ldN <= 128)) return s;
   return 0;
@@ -1885,21 +1564,15 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
   const unsigned spin_limit = mc_spin_limit();
   const dim3 grid(MC_XCDS * K), block(MC_THREADS);
   const int hops = mc_hops(K, S);
-  // Z-slice issue point (FS_MIX_MC_ZAT=0|1|2 for diagnostics): after the exchange by default --
-  // r02i, us per step, (hops, ZAT) = (1, 0) / (2, 0) / (2, 1) / (2, 2): N = 1000, C = 10, K = 32:
-  // 6.61 / 6.03 / 5.45 / 5.44; N = 300, C = 4, K = 19: 4.33 / 4.34 / 4.08 / 3.38
+  // the next Z slice is issued after the exchange -- r02i, us per step, (hops, issued at the top /
+  // after hop 1 / after the exchange): N = 1000, C = 10, K = 32: (1, top) 6.61, (2, top) 6.03,
+  // (2, hop 1) 5.45, (2, exchange) 5.44; N = 300, C = 4, K = 19: 4.33 / 4.34 / 4.08 / 3.38
   if (pf.prog) pf.h = std::min(pf.h, (MC_XCDS - 1) * K);   // helpers: the grid's other-XCD blocks
-  const char* zenv = getenv("FS_MIX_MC_ZAT");
-  const int zat = zenv ? std::min(2, std::max(0, atoi(zenv))) : 2;
-#define MC_CASE(S_, H_, Z_)                                                                                   \
-  if (S == S_ && hops == H_ && zat == Z_)                                                                     \
-    hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_, Z_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr, \
+#define MC_CASE(S_, H_)                                                                                       \
+  if (S == S_ && hops == H_)                                                                                  \
+    hipLaunchKernelGGL((mix_solve_mc_kernel<S_, H_>), grid, block, 0, st, Z, y, perms, N, C, nv, epochs, Bv, lr,  \
                        mom, p, buf, first, ws, err, K, spin_limit, pf.prog, pf.h, pf.lead);
-#define MC_CASES(Z_) \
-  MC_CASE(8, 1, Z_) MC_CASE(16, 1, Z_) MC_CASE(32, 1, Z_) MC_CASE(64, 1, Z_) \
-  MC_CASE(8, 2, Z_) MC_CASE(16, 2, Z_) MC_CASE(32, 2, Z_) MC_CASE(64, 2, Z_)
-  MC_CASES(0) MC_CASES(1) MC_CASES(2)
-#undef MC_CASES
+  MC_CASE(8, 1) MC_CASE(16, 2) MC_CASE(32, 2) MC_CASE(64, 2)
 #undef MC_CASE
   return 0;
 }
@@ -2119,11 +1792,9 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
   }
 }
 
-// clients per lane: 8 (128 per workgroup) for C <= 10, else 4; FS_MIX_QMC_NK=4 forces 4 (diagnostics)
-static int qmc_nk(int C) {
-  const char* e = getenv("FS_MIX_QMC_NK");
-  return (C <= 10 && !(e && atoi(e) == 4)) ? 8 : 4;
-}
+// clients per lane: 8 (128 per workgroup) for C <= 10, else 4 (r02s2qmc2: NK = 4, K = 16 at
+// N = 1000 measured the same 3.8 us per step as NK = 8, K = 8)
+static int qmc_nk(int C) { return C <= 10 ? 8 : 4; }
 
 static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
   const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
@@ -2175,8 +1846,9 @@ extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   const int S = mc_slice(N);
   const int K = S ? (mix_ldn(N) + S - 1) / S : 0;
   const int64_t mc = mc_covers(N, C, Bv) ? mc_xbytes(K) : 0;
-  const int64_t rows = mrr_covers(N, C, Bv) ? mrr_xbytes(N) : 0;
-  return std::max(mc, rows) + MC_ERR_BYTES;
+  const int nk = qmc_nk(C);
+  const int64_t qmc = mc_xbytes((mix_ldn(N) + 16 * nk - 1) / (16 * nk));
+  return std::max(mc, (N > 128 && C <= 16 && Bv <= 16) ? qmc : (int64_t)0) + MC_ERR_BYTES;
 }
 
 extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val, float* d_Z,
@@ -2199,32 +1871,32 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
   FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
   hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
-  // solver choice: FS_MIX_SOLVER=auto (default) | reg2 | reg | mc | staged | global (diagnostics
-  // and tests; a forced solver that does not cover the shape falls through to the next one)
-  const char* pick = getenv("FS_MIX_SOLVER");
-  const std::string want = pick ? pick : "auto";
+  // solver choice: by shape, or forced by fs_tuning.mix_solver (tests, diagnostics; a forced
+  // solver that does not cover the shape falls through to the next one)
+  const fs_tuning tune = tuning();
+  const int want = tune.mix_solver;
+  const bool aut = want == FS_SOLVER_AUTO;
   // one wave where it measured fastest (N <= 16, C = 3..4: 0.616 vs 0.62 us per step); the
   // quarter-wave solver from C <= 2 (config 1, N = 10: 0.574 vs 0.617 us, r02s2c1b) upwards
   const bool auto_wave = N <= 16 && C >= 3 && C <= 4 && Bv <= 16;
-  const bool use_quad = (want == "auto" && !auto_wave && quad_covers(N, C, Bv, n_val, epochs)) || want == "quad";
+  const bool use_quad = (aut && !auto_wave && quad_covers(N, C, Bv, n_val, epochs)) || want == FS_SOLVER_QUAD;
   // the multi-CU quarter-wave solver where the single-workgroup register solvers end (N > 256)
-  const bool use_qmc = want == "qmc" || (want == "auto" && N > 256 && qmc_covers(N, C, Bv, n_val, epochs));
+  const bool use_qmc = want == FS_SOLVER_QMC || (aut && N > 256 && qmc_covers(N, C, Bv, n_val, epochs));
   MixPrefetch pf{nullptr, 0, 0};
   {
-    // L2 prefetch helpers of the single-CU solvers: FS_MIX_PF_H helper workgroups (0 = off;
-    // default 4 for the quarter-wave solver, whose gather they speed up: r02s2k, 1.42-1.47 ->
-    // 1.35-1.43 us per step at config 2; 0 for the others, where they measured nothing),
-    // FS_MIX_PF_LEAD steps ahead; the progress word lives in the error block (byte 128)
-    const char* eh = getenv("FS_MIX_PF_H");
-    const char* el = getenv("FS_MIX_PF_LEAD");
+    // L2 prefetch helpers (fs_tuning.mix_prefetch: 0 = by solver, -1 = none, n): 4 for the
+    // quarter-wave solver, whose gather they speed up (r02s2k, 1.42-1.47 -> 1.35-1.43 us per step
+    // at config 2), 16 for qmc, none for the others, where they measured nothing; they run
+    // mix_prefetch_lead (0: 16) steps ahead; the progress word lives in the error block (byte 128)
     // (quad: only when Z outgrows the L2s -- at config 1's 0.6 MB the helpers cost 3 %, r02s2c1)
     const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
-    const int h = eh ? std::max(0, std::min(224, atoi(eh))) : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0));
+    const int h = tune.mix_prefetch > 0 ? tune.mix_prefetch
+                  : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0)));
     // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
     // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
     // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
     // 16 is still the fastest: 3.85 us per step vs 4.75 at leads 2-4 (r02s2lead)
-    const int lead = el ? std::max(1, atoi(el)) : 16;
+    const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : 16;
     if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
       pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
       pf.h = h;
@@ -2233,13 +1905,13 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
       if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
     }
   }
-  // auto: one wave for N <= 16, C <= 4; the quarter-wave solver (+ L2 prefetch helpers) for
+  // by shape: one wave for N <= 16, C <= 4; the quarter-wave solver (+ L2 prefetch helpers) for
   // N <= 64, C <= 16 or N <= 128, C <= 10; the register solvers where an instance covers the
   // shape (no cross-CU exchange: ~1-2.5 us per step); for N > 256 the multi-CU quarter-wave
   // solver (one exchange hop per step; 3.9 us at N = 1000, C = 10) where it covers, else the
   // multi-CU solver (two hops, ~4-7 us per step, 7-11x the single-workgroup staged / global
   // solvers at N = 200..1000, C = 10); else those.
-  if (((want == "auto" && auto_wave) || want == "wave") && N <= 16 && C <= 4 && Bv <= 16) {
+  if (((aut && auto_wave) || want == FS_SOLVER_WAVE) && N <= 16 && C <= 4 && Bv <= 16) {
     hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
                        Bv, lr_p, momentum, d_p, d_buf, d_first);
     t_last_solver = 6;
@@ -2254,28 +1926,18 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   }
   // form 2 (two rows per wave) where it measured faster: N in (128, 256], NK = 4 (2.0 vs 4.1 us
   // per step at N = 256, C = 4); below that the one-row form is as fast or faster (r02g)
-  if (((want == "auto" && N > 128) || want == "reg2") &&
+  if (((aut && N > 128) || want == FS_SOLVER_REG2) &&
       mix_solve_reg2(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first)) {
     t_last_solver = 5;
     FS_LAUNCH_CHECK();
     return FS_OK;
   }
-  if ((want == "auto" || want == "reg") &&
+  if ((aut || want == FS_SOLVER_REG) &&
       mix_solve_reg(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf, d_first,
                     pf)) {
     t_last_solver = 1;
     FS_LAUNCH_CHECK();
     return FS_OK;
-  }
-  if (want == "rows") {
-    const int rc = mix_solve_rows(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
-                                  d_first, d_ws, ws_bytes, MC_ERR_BYTES);
-    if (rc < 0) return rc;
-    if (rc == 1) {
-      t_last_solver = 7;
-      FS_LAUNCH_CHECK();
-      return FS_OK;
-    }
   }
   if (use_qmc) {
     const int rc = mix_solve_qmc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
@@ -2287,7 +1949,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
       return FS_OK;
     }
   }
-  if (want == "auto" || want == "mc") {
+  if (aut || want == FS_SOLVER_MC) {
     const int rc = mix_solve_mc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
                                 d_first, d_ws, ws_bytes, pf);
     if (rc < 0) return rc;
@@ -2301,7 +1963,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
     // LDS-staged solver: two batches of Z rows + p, buf and the wave partials must fit
     const int CN4 = C * mix_ldn(N);
     const size_t lds2 = sizeof(float) * (2 * (size_t)Bv * CN4 + 2 * (size_t)N + (size_t)MS_WAVES * N);
-    if (want != "global" && N <= 64 * MS2_NK && C <= 16 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
+    if (want != FS_SOLVER_GLOBAL && N <= 64 * MS2_NK && C <= 16 && lds2 <= 150 * 1024 && (size_t)Bv * (CN4 / 4) <= (size_t)MS_THREADS * MS2_PER_THREAD) {
       const void* kfn = reinterpret_cast<const void*>(&mix_solve_staged_kernel<16>);
       if (lds2 > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);

@@ -254,10 +254,9 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
     p->max_client_steps = std::max<int64_t>(1, (int64_t)d.E * ((mx + d.B - 1) / std::max(1, d.B)));
   }
   // FS_PHASE_EVAL_DEFER: a parallel split launch that leaves CUs idle evaluates the previous
-  // round's global model on them (FS_EVAL_FUSE=0 turns this off)
+  // round's global model on them (fs_tuning.no_eval_fuse turns this off)
   if (d.d_phi_t && d.n_t > 0 && d.d_labels_t && d.d_eval_ws && d.C <= 16 && d.G > 1 && !d.chained) {
-    const char* ev = std::getenv("FS_EVAL_FUSE");
-    if (!(ev && std::atoi(ev) == 0)) {
+    if (!fs::tuning().no_eval_fuse) {
       const int idle = fs::split_idle_cus(d.N, d.C, d.B, d.ld, d.G, 0);
       p->fuse_E = (int)std::min<int64_t>(idle, (d.n_t + 15) / 16);
     }
@@ -270,17 +269,15 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p->d_perm[s]), sizeof(int32_t) * p->perm_len);
     // ordering-only events: no timestamps and no system-scope release when they complete (the
     // waits are device-side, and the host only needs the seed upload's completion, not the
-    // visibility of device writes) -- FS_EVENT_FENCE=1 restores the default release
-    const char* ef = getenv("FS_EVENT_FENCE");
-    const unsigned evf = hipEventDisableTiming | ((ef && atoi(ef) == 1) ? 0u : (unsigned)hipEventDisableSystemFence);
+    // visibility of device writes)
+    const unsigned evf = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->uploaded[s], evf);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&p->consumed[s], evf);
   }
   if (d.shuffle_device) {
     // the seeds stay in pinned, coherent host memory that the shuffle kernel reads directly
-    // (FS_SEED_COPY=1: upload them with hipMemcpyAsync instead)
-    const char* sc = getenv("FS_SEED_COPY");
-    p->seed_copy = sc && atoi(sc) == 1;
+    // (round 2, r02s2: no slower than a hipMemcpyAsync upload, and no copy on the side stream)
+    p->seed_copy = false;
     for (int k = 0; k < fs_plan::SEED_SLOTS && e == hipSuccess; ++k) {
       e = hipHostMalloc(reinterpret_cast<void**>(&p->h_seed[k]), sizeof(int64_t) * std::max<int64_t>(1, P),
                         p->seed_copy ? hipHostMallocDefault : (hipHostMallocMapped | hipHostMallocCoherent));
@@ -318,28 +315,16 @@ extern "C" int fs_plan_create(const fs_plan_desc* desc, fs_plan** out) {
 }
 
 // Device replay: upload the seeds and launch fs_randperm_device on the side stream.
-static double now_us() {
-  return 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                    std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
   const int s = t & 1;
   const int64_t P = (int64_t)p->n.size();
-  static const bool trace = getenv("FS_PLAN_TRACE") && atoi(getenv("FS_PLAN_TRACE")) == 1;   // diagnostics
-  double t0 = trace ? now_us() : 0.0, t1 = 0.0, t2 = 0.0;
   const int k = t % fs_plan::SEED_SLOTS;
   if (p->seed_pending[k]) FS_HIP(hipEventSynchronize(p->seed_read[k]), "fs_plan_shuffle");   // pinned seeds free
-  if (trace) t1 = now_us();
   std::memcpy(p->h_seed[k], h_seeds, sizeof(int64_t) * P);
   if (p->cons_recorded[s]) FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s], 0), "fs_plan_shuffle");
   // optionally also behind the latest local training (the other slot's consumer)
   if (p->d.shuffle_after_train && p->cons_recorded[s ^ 1])
     FS_HIP(hipStreamWaitEvent(p->copy, p->consumed[s ^ 1], 0), "fs_plan_shuffle");
-  if (trace) {
-    t2 = now_us();
-    fprintf(stderr, "fs_plan_shuffle t=%d: seed-slot wait %.1f us, stream wait %.1f us\n", t, t1 - t0, t2 - t1);
-  }
   if (p->seed_copy)
     FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
            "fs_plan_shuffle");
@@ -451,9 +436,7 @@ static int chunk_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
 extern "C" int fs_timer_create(void** ev) {
   FS_REQUIRE(ev, "null pointer");
   hipEvent_t e = nullptr;
-  const char* f = getenv("FS_TIMER_FLAGS");        // diagnostics: raw hipEventCreateWithFlags flags
-  FS_HIP(hipEventCreateWithFlags(&e, f ? (unsigned)strtoul(f, nullptr, 0) : (unsigned)hipEventDisableSystemFence),
-         "fs_timer_create");
+  FS_HIP(hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence), "fs_timer_create");
   *ev = e;
   return FS_OK;
 }

@@ -30,7 +30,6 @@ All arithmetic of the round runs in the gfx950 kernels of libfedsim.so; there is
 CPU path.  ``type`` must be 'classification' (the reference's MSE branch,
 tools.py:183-184, is not on the benchmarked path).
 """
-import os
 
 import numpy as np
 import torch
@@ -102,13 +101,32 @@ def _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round,
         _check_labels([y_val], num_classes, 'validation')
 
 
+# scheduling options of a Federation (how the launches of the rounds are arranged; none of
+# them changes a result bit):
+#   shuffle_chunk   FedAvg / FedProx with device-replayed shuffles: the shuffles of this many
+#                   rounds come from one launch, one chunk ahead (1 = per round)
+#   defer_eval      round t's test evaluation rides on round t+1's training launch where that
+#                   launch leaves CUs idle (FS_PHASE_EVAL_DEFER)
+#   fedamw_shuffle  'early': FedAMW's round t+1 shuffles run beside the Z GEMM; 'late': after
+#                   the round, beside the p-solve
+OPTIONS = {'shuffle_chunk': 8, 'defer_eval': True, 'fedamw_shuffle': 'early'}
+
+
 class Federation:
     """One algorithm call split into setup / rounds / results (bench.py drives the
     rounds one at a time through the same code path as the drop-ins)."""
 
     def __init__(self, algo, X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
                  batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=None, verbose=True,
-                 shuffle_device=True):
+                 shuffle_device=True, options=None):
+        opts = dict(OPTIONS)
+        for k, v in (options or {}).items():
+            if k not in opts:
+                raise ValueError('unknown Federation option %r (known: %s)' % (k, ', '.join(sorted(OPTIONS))))
+            opts[k] = v
+        if opts['fedamw_shuffle'] not in ('early', 'late'):
+            raise ValueError("fedamw_shuffle must be 'early' or 'late'")
+        self.options = opts
         # (training labels: only this rank's clients, below -- in sharded mode the other ranks'
         # entries of X_train / y_train need only have the right lengths)
         _check_inputs(type, X_train, y_train, num_classes, batch_size, epoch, round, y_test,
@@ -193,18 +211,17 @@ class Federation:
         # round t's local training, beside its p-solve (one to 32 CUs busy), not beside the
         # training kernel, whose groups would wait for the CUs they hold
         # FedAvg / FedProx with device-replayed shuffles: generate them K rounds per launch
-        # (FS_SHUFFLE_CHUNK, default 8; 1 = per round), one chunk ahead of the rounds that use
-        # them, so consecutive rounds run with no cross-stream wait between them.  FedAMW keeps
-        # per-round shuffles (its validation shuffles are double-buffered per round).
-        env_k = os.environ.get('FS_SHUFFLE_CHUNK')
+        # (options['shuffle_chunk'], default 8; 1 = per round), one chunk ahead of the rounds that
+        # use them, so consecutive rounds run with no cross-stream wait between them.  FedAMW
+        # keeps per-round shuffles (its validation shuffles are double-buffered per round).
         self.chunk = 1
         if self.mixture is None and shuffle_device:
-            self.chunk = max(1, min(int(env_k) if env_k else 8, R))
+            self.chunk = max(1, min(int(opts['shuffle_chunk']), R))
             if self.chunk > 1:
                 self.plan.set_chunk(self.chunk)
         # round t's test-set evaluation is deferred into round t+1's training launch when that
-        # launch leaves CUs idle (FS_EVAL_DEFER=0: an evaluation launch per round)
-        self.defer_eval = os.environ.get('FS_EVAL_DEFER', '1') != '0'
+        # launch leaves CUs idle (options['defer_eval'] = False: an evaluation launch per round)
+        self.defer_eval = bool(opts['defer_eval'])
         self._prepared = 0              # next round whose shuffles are to be prepared
         self._train_done = None
         self.t = 0
@@ -264,8 +281,8 @@ class Federation:
             # FedAMW: round t+1's shuffles are enqueued now (nothing else draws from the global
             # generator in between, so the draw order is unchanged) and the p-solve waits for the
             # validation shuffles: they run beside the Z GEMM, not on the CUs of the p-solve's
-            # workgroups (FS_FEDAMW_SHUFFLE=late: after the round, beside the p-solve)
-            early = self.t + 1 < self.R and os.environ.get('FS_FEDAMW_SHUFFLE', 'early') != 'late'
+            # workgroups (options['fedamw_shuffle'] = 'late': after the round, beside the p-solve)
+            early = self.t + 1 < self.R and self.options['fedamw_shuffle'] != 'late'
             if early:
                 self._prepare_upto(t + 2)
         if self.zshard:
@@ -336,8 +353,8 @@ class Federation:
         return train_loss, test_loss, test_acc
 
 
-def _run(algo, *args, stats=None, verbose=True):
-    fed = Federation(algo, *args, stats=stats, verbose=verbose)
+def _run(algo, *args, stats=None, verbose=True, options=None):
+    fed = Federation(algo, *args, stats=stats, verbose=verbose, options=options)
     for _ in range(fed.R):
         fed.round()
     return fed.results()
@@ -345,27 +362,30 @@ def _run(algo, *args, stats=None, verbose=True):
 
 def FedAvg(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01, epoch=2,
            batch_size=32, prox=False, mu=0.1, lambda_reg_if=False, lambda_reg=0.01, round=100, *,
-           clients='sequential', stats=None, verbose=True):
-    """tools.py:329-353."""
+           clients='sequential', stats=None, verbose=True, options=None):
+    """tools.py:329-353.  ``options``: launch-scheduling options (``OPTIONS``)."""
     return _run('fedavg', X_train, y_train, X_test, y_test, None, type, num_classes, D, lr, epoch, batch_size,
-                prox, mu, lambda_reg_if, lambda_reg, round, None, clients, stats=stats, verbose=verbose)
+                prox, mu, lambda_reg_if, lambda_reg, round, None, clients, stats=stats, verbose=verbose,
+                options=options)
 
 
 def FedProx(X_train, y_train, X_test, y_test, type='classification', num_classes=10, D=200, lr=0.01, epoch=2,
             batch_size=32, prox=True, mu=0.1, lambda_reg_if=False, lambda_reg=0.01, round=100, *,
-            clients='sequential', stats=None, verbose=True):
+            clients='sequential', stats=None, verbose=True, options=None):
     """tools.py:356-380 (FedAvg with the proximal term on by default)."""
     return _run('fedprox', X_train, y_train, X_test, y_test, None, type, num_classes, D, lr, epoch, batch_size,
-                prox, mu, lambda_reg_if, lambda_reg, round, None, clients, stats=stats, verbose=verbose)
+                prox, mu, lambda_reg_if, lambda_reg, round, None, clients, stats=stats, verbose=verbose,
+                options=options)
 
 
 def FedAMW(X_train, y_train, X_test, y_test, validloader, type='classification', num_classes=10, D=200, lr=0.01,
            epoch=2, batch_size=32, prox=False, mu=0.1, lambda_reg_if=True, lambda_reg=0.01, round=100, lr_p=5e-5,
-           *, clients='sequential', stats=None, verbose=True):
+           *, clients='sequential', stats=None, verbose=True, options=None):
     """tools.py:413-463: FedAvg-style round + learned mixture weights p (SGD momentum 0.9
     on the pooled validation set, ``round`` inner epochs per round), aggregate with p."""
     return _run('fedamw', X_train, y_train, X_test, y_test, validloader, type, num_classes, D, lr, epoch,
-                batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=stats, verbose=verbose)
+                batch_size, prox, mu, lambda_reg_if, lambda_reg, round, lr_p, clients, stats=stats, verbose=verbose,
+                options=options)
 
 
 # --------------------------------------------------------------------------- #

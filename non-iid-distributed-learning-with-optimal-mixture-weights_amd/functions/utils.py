@@ -153,7 +153,9 @@ def load_full_data(dataset_name, num_partitions=10, alpha=0.1, root_dir='../FedA
     path = os.path.join(root_dir, dataset_name)
     if os.path.exists(path):
         X, y, zb, d = read_libsvm(path)
-        Xt, yt, _, _ = read_libsvm(path + '.t', n_features=d, zero_based=zb)
+        # each file picks its own index base, as the reference's two load_svmlight_file calls
+        # do ('auto'); the test file keeps the training width
+        Xt, yt, _, _ = read_libsvm(path + '.t', n_features=d, zero_based=-1)
         y, yt = svmlight_labels(y, dataset_name), svmlight_labels(yt, dataset_name)
     else:
         X, y, Xt, yt = synthetic_libsvm(dataset_name, **(synth or {}))

@@ -9,6 +9,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 ROUND_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'fed*.npz')))
 TRAIN_UNITS = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'unit_train_*.npz')))
 LONG_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'long_fed*.npz')))
+BENCH_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, 'bench_fedamw_*.npz')))
 
 
 def load(name):
@@ -20,6 +21,15 @@ def load_long(name):
     """A long-horizon case: the shared inputs (long_data.npz) merged with the case's
     hyper-parameters and reference outputs; ``W`` holds the global model at rounds ``snap``."""
     d = load('long_data')
+    d.update(load(name))
+    return d
+
+
+def load_bench(name):
+    """A benchmark-length FedAMW case (config 2's N = 100, C = 10; n_v >= 2,000, R = 34: >= 5,000
+    p-SGD steps per round): bench_data.npz merged with the case; ``W`` at rounds ``snap``,
+    ``p`` after every round."""
+    d = load('bench_data')
     d.update(load(name))
     return d
 

@@ -25,6 +25,17 @@ Long-horizon fixtures (``long_*.npz``, inputs in ``long_data.npz``): FedProx and
 chained and parallel clients, D = 1024, C = 10, R = 20 rounds (fp32 drift over many
 rounds pinned to the reference; exp.py:31-36 runs D = 2000, R = 100).
 
+Benchmark-length FedAMW fixtures (``bench_fedamw_*.npz``, inputs in ``bench_data.npz``):
+config 2's client count and classes (N = 100, C = 10) with a pooled validation set of
+n_v >= 2,000 rows and R = 34 rounds, so every round runs R * ceil(n_v / 16) >= 5,000
+dependent momentum steps of the p-SGD (tools.py:441-453), chained and parallel clients.
+
+exp.py's own sequence (``exp_satimage.npz``): exp.py:60-130 on ONE un-reseeded stream -- the
+reference's load_full_data on synthetic satimage-shaped LIBSVM files, the restated lines
+61-99, then the six algorithm calls in exp.py's order with exp.py's positional arguments
+(get_parameter('satimage')) -- recording every return, the heterogeneity and where both
+global generators are left.
+
 Data-preparation fixtures (``prep_*.npz``): exp.py:60-99 run through the reference's own
 ``functions/utils.py`` (``load_full_data`` -> ``svmlight_data`` +
 ``get_Dirichlet_distribution``) on synthetic LIBSVM files written here, with two
@@ -377,6 +388,53 @@ def run_long():
         print(name, 'acc', np.round(ta.numpy()[LONG_SNAP], 2), 'loss', np.round(tr.detach().numpy()[LONG_SNAP], 4))
 
 
+BENCH_R = 34
+BENCH_SNAP = [0, 8, 16, 24, 33]
+BENCH_CASES = [
+    ('bench_fedamw_seq', 'seq'),
+    ('bench_fedamw_par', 'par'),
+]
+BENCH_HP = dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=BENCH_R, lr_p=3e-4)
+
+
+def run_bench(modes=('seq', 'par')):
+    """FedAMW at config 2's N and C over R = 34 rounds with n_v >= 2,000: >= 5,000 p-SGD steps
+    per round (D = 32 keeps the fixture small; the p-solve's work is N x C x n_v).  lr_p = 3e-4:
+    at 1e-3 the unconstrained p of the parallel-clients run diverges after ~30 rounds (the
+    reference's own output turns NaN), where no fp32 restatement can follow it."""
+    rs = np.random.RandomState(41)
+    sizes = list(rs.randint(100, 151, size=100))
+    d = synth(seed=41, sizes=sizes, n_test=200, n_raw=12, D=32, C=10, val_frac=0.2)
+    nv = len(d['y_val'])
+    assert nv >= 2000 and BENCH_R * ((nv + 15) // 16) >= 5000, nv
+    np.savez_compressed(os.path.join(OUT, 'bench_data.npz'), **d, torch_seed=TORCH_SEED, C=10, D=32,
+                        snap=np.array(BENCH_SNAP))
+    Xs, ys, Xt, yt = _split(d)
+    vl = torch.utils.data.DataLoader(
+        torch.utils.data.TensorDataset(torch.from_numpy(d['X_val']), torch.from_numpy(d['y_val'])),
+        batch_size=16, shuffle=True)
+    hp = BENCH_HP
+    torch.set_num_threads(1)           # (tiny per-step ops: one thread is ~8x faster here, same values)
+    pos = ('classification', 10, 32, hp['lr'], hp['epoch'], hp['batch_size'], hp['prox'], hp['mu'], hp['reg'],
+           hp['lam'], hp['R'])
+    for name, mode in BENCH_CASES:
+        if mode not in modes:
+            continue
+        _trace['W'].clear()
+        _trace['p'].clear()
+        torch.manual_seed(TORCH_SEED)
+        with contextlib.redirect_stdout(io.StringIO()):
+            tr, tl, ta = {'seq': T.FedAMW, 'par': _fedamw_par}[mode](Xs, ys, Xt, yt, vl, *pos, hp['lr_p'])
+        rec = {k: np.asarray(v) for k, v in hp.items()}
+        rec.update(algo='fedamw', mode=mode, train_loss=tr.detach().numpy(), test_loss=tl.numpy(),
+                   test_acc=ta.numpy(), W=np.stack(_trace['W'])[BENCH_SNAP], snap=np.array(BENCH_SNAP),
+                   p=np.stack(_trace['p']), n_val=nv,
+                   rng_after=torch.empty(4, dtype=torch.int64).random_().numpy())
+        np.savez_compressed(os.path.join(OUT, name + '.npz'), **rec)
+        print(name, 'n_val', nv, 'steps/round', BENCH_R * ((nv + 15) // 16), 'acc',
+              np.round(ta.numpy()[BENCH_SNAP], 2), 'p range', float(rec['p'].min()), float(rec['p'].max()))
+
+
 def _reference_utils():
     """Import /root/reference/functions/utils.py with the two stand-ins described above."""
     import types
@@ -480,8 +538,105 @@ def run_prep():
         print('dirichlet', name, lens(pr)[:10])
 
 
+EXP = dict(dataset='satimage', n=900, nt=240, D=64, N=5, alpha=0.3, local_epoch=2, Round=3, batch_size=32)
+
+
+def run_exp():
+    """exp.py:28-130 on one stream: seeds, the reference's load_full_data on synthetic
+    satimage-shaped LIBSVM files (36 dense columns in [0, 1], labels 1..6), the restated lines
+    61-99, then Centralized, Distributed, FedAMW_OneShot, FedAvg, FedProx, FedAMW called
+    positionally with exp.py's arguments and get_parameter('satimage'), no reseeding."""
+    import shutil
+    import tempfile
+    from sklearn.datasets import dump_svmlight_file
+    from functions.optimal_parameters import get_parameter
+    U = _reference_utils()
+    e = EXP
+    rs = np.random.RandomState(88)
+    proto = rs.rand(6, 36)
+    yy = rs.randint(1, 7, size=e['n'] + e['nt'])
+    X = np.clip(proto[yy - 1] + 0.35 * rs.normal(size=(len(yy), 36)), 0, 1).astype(np.float32)
+    X[:, 35] = np.maximum(X[:, 35], 0.01)          # the last column populated: equal file widths
+    y, yt = yy[:e['n']].astype(np.float64), yy[e['n']:].astype(np.float64)
+    X, Xt = X[:e['n']], X[e['n']:]
+    P = get_parameter(e['dataset'])
+    D, N, R, le, B = e['D'], e['N'], e['Round'], e['local_epoch'], e['batch_size']
+    tmp = tempfile.mkdtemp()
+    cwd = os.getcwd()
+    res = {}
+    try:
+        os.makedirs(os.path.join(tmp, 'FedAMW', 'datasets'))
+        os.makedirs(os.path.join(tmp, 'work'))
+        dump_svmlight_file(X, y, os.path.join(tmp, 'FedAMW', 'datasets', e['dataset']), zero_based=False)
+        dump_svmlight_file(Xt, yt, os.path.join(tmp, 'FedAMW', 'datasets', e['dataset'] + '.t'), zero_based=False)
+        os.chdir(os.path.join(tmp, 'work'))              # utils.py:37 reads '../FedAMW/datasets/'
+        torch.manual_seed(100)                            # exp.py:28-29
+        np.random.seed(100)
+        with contextlib.redirect_stdout(io.StringIO()):
+            trainloader, testloader, parts, d, C = U.load_full_data(e['dataset'], N, e['alpha'])
+            # exp.py:61-99 (restated: iter(loader).next() -> next(iter(loader)))
+            X_train, y_train_all = next(iter(trainloader))
+            X_test, y_test = next(iter(testloader))
+            X_train_FM_all, X_test_FM = T.feature_mapping(X_train.reshape(1, X_train.shape[0], X_train.shape[1]),
+                                                          X_test, P['kernel_par'], D, P['kernel_type'])
+            X_train_FM_all = X_train_FM_all.reshape(-1, D)
+            data_hete = 0
+            Cm = torch.matmul(X_train_FM_all.T, X_train_FM_all) / len(X_train_FM_all)
+            X_train_FM, y_train = [], []
+            for idx in parts:
+                X_train_FM.append(X_train_FM_all[idx, :])
+                y_train.append(y_train_all[idx])
+                Cj = torch.matmul(X_train_FM[-1].T, X_train_FM[-1]) / len(X_train_FM[-1])
+                data_hete += len(X_train_FM[-1]) / len(X_train_FM_all) * torch.norm(Cm - Cj)
+            X_val_all, y_val_all, X_tr_all, y_tr_all = [], [], [], []
+            for i in range(N):
+                random_idx = np.arange(X_train_FM[i].shape[0])
+                np.random.shuffle(random_idx)
+                th = int(X_train_FM[i].shape[0] * 0.2)
+                X_val_all.append(X_train_FM[i][random_idx[:th]])
+                y_val_all.append(y_train[i][random_idx[:th]])
+                X_tr_all.append(X_train_FM[i][random_idx[th:]])
+                y_tr_all.append(y_train[i][random_idx[th:]])
+            X_val, y_val = torch.cat(X_val_all, 0), torch.cat(y_val_all, 0)
+            vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(X_val, y_val), batch_size=16,
+                                             shuffle=True)
+            a = (X_tr_all, y_tr_all, X_test_FM, y_test)
+            task, lr = P['task_type'], P['lr']
+            # exp.py:102-130, positional, in order, on the same stream
+            res['CL'] = T.Centralized(*a, task, C, D, lr, le * R, B, False, 0, False, 0)
+            res['DL'] = T.Distributed(*a, task, C, D, lr, le * R, B, False, 0, False, 0)
+            res['FedAMW_OneShot'] = T.FedAMW_OneShot(*a, vl, task, C, D, lr, le * R, B, False, 0, True,
+                                                     P['lambda_reg_os'], R, P['lr_p_os'])
+            res['FedAvg'] = T.FedAvg(*a, task, C, D, lr, le, B, False, 0, False, 0, R)
+            res['FedProx'] = T.FedProx(*a, task, C, D, lr, le, B, True, P['lambda_prox'], False, 0, R)
+            res['FedAMW'] = T.FedAMW(*a, vl, task, C, D, lr, le, B, False, 0, True, P['lambda_reg'], R, P['lr_p'])
+        after_torch = torch.empty(4, dtype=torch.int64).random_().numpy()
+        after_np = np.random.randint(0, 1 << 30, 4)
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+    names = ['CL', 'DL', 'FedAMW_OneShot', 'FedAvg', 'FedProx', 'FedAMW']
+    mats = {k: np.empty((6, R)) for k in ('train_loss', 'test_loss', 'test_acc')}
+    f = lambda v: np.asarray(v.detach().numpy() if isinstance(v, torch.Tensor) else v, dtype=np.float64)
+    for k, nm in enumerate(names):      # exp.py:104-129: scalars broadcast over the rounds
+        for j, key in enumerate(('train_loss', 'test_loss', 'test_acc')):
+            mats[key][k, :] = f(res[nm][j])
+    rec = dict(X=X, y=y, X_test=Xt, y_test=yt, heterogeneity=np.float64(data_hete.item()), after_torch=after_torch,
+               after_np=after_np, C=C, d=d, parts_len=np.array([len(p) for p in parts]), **mats,
+               **{k: (v if isinstance(v, str) else np.asarray(v)) for k, v in EXP.items()})
+    np.savez_compressed(os.path.join(OUT, 'exp_satimage.npz'), **rec)
+    print('exp_satimage hete', float(data_hete), 'final acc', mats['test_acc'][:, -1])
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params', 'long', 'prep']
+    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params', 'long', 'prep', 'bench', 'exp']
+    if 'bench' in which:
+        run_bench()
+    for m in ('seq', 'par'):
+        if 'bench:' + m in which:
+            run_bench((m,))
+    if 'exp' in which:
+        run_exp()
     if 'long' in which:
         run_long()
     if 'prep' in which:

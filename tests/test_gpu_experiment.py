@@ -128,3 +128,29 @@ def test_experiment_end_to_end(amd, tmp_path):
         saved = pickle.load(f)
     assert saved['epochs'] == 3 and saved['heterogeneity'].shape == (1,)
     assert ((out['test_acc'] >= 0) & (out['test_acc'] <= 100)).all()
+
+
+def test_experiment_matches_reference_sequence(amd, tmp_path):
+    """exp.py's whole sequence on ONE un-reseeded stream (exp_satimage.npz: the reference's
+    load_full_data on the same LIBSVM files, exp.py:61-99 restated, then its six algorithm calls
+    in order with get_parameter('satimage')): every returned loss / accuracy of the six
+    algorithms, the heterogeneity and where both global generators end up -- so the stream
+    continuity across the calls is pinned, not just each call after a reseed."""
+    from sklearn.datasets import dump_svmlight_file
+    from tests.fixtures import LOSS_RTOL, load
+    d = load('exp_satimage')
+    root = tmp_path / 'datasets'
+    root.mkdir()
+    name = str(d['dataset'])
+    dump_svmlight_file(d['X'], d['y'], str(root / name), zero_based=False)
+    dump_svmlight_file(d['X_test'], d['y_test'], str(root / (name + '.t')), zero_based=False)
+    out = amd.experiment.run(name, D=int(d['D']), num_partitions=int(d['N']), local_epoch=int(d['local_epoch']),
+                             Round=int(d['Round']), batch_size=int(d['batch_size']), n_repeats=1,
+                             alpha_Dirk=float(d['alpha']), data_dir=str(root) + '/', save=False, verbose=False)
+    np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['after_torch'])
+    np.testing.assert_array_equal(np.random.randint(0, 1 << 30, 4), d['after_np'])
+    assert abs(out['heterogeneity'][0] - float(d['heterogeneity'])) <= 1e-4 * abs(float(d['heterogeneity']))
+    for key in ('train_loss', 'test_loss'):
+        got, ref = out[key][:, :, 0], d[key]
+        np.testing.assert_allclose(got, ref, rtol=0, atol=LOSS_RTOL * max(1.0, np.abs(ref).max()), err_msg=key)
+    assert np.abs(out['test_acc'][:, :, 0] - d['test_acc']).max() <= 100.0 / len(d['y_test']) + 1e-4

@@ -8,8 +8,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
-                            load_long, positional, split_clients)
+from tests.fixtures import (BENCH_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol,
+                            load, load_bench, load_long, positional, split_clients)
 
 pytestmark = pytest.mark.gpu
 
@@ -83,45 +83,79 @@ def test_dropin_long_horizon_golden(amd, name):
         assert np.abs(stats['p'].cpu().numpy() - d['p'][-1]).max() <= P_RTOL * np.abs(d['p']).max()
 
 
-@pytest.mark.parametrize('chunk', ['1', '3', '7'])
+@pytest.mark.parametrize('name', BENCH_CASES)
+def test_dropin_benchmark_length_fedamw(amd, name):
+    """The FedAMW drop-in at config 2's N = 100, C = 10 (the quarter-wave p-solver config 2's
+    leg runs) with >= 5,000 dependent p-SGD steps per round over R = 34 rounds, chained and
+    parallel clients, against the reference: global models at the snapshot rounds, the final
+    mixture weights, losses and accuracy within the stated fp32 tolerances."""
+    d = load_bench(name)
+    (tr, tl, ta), stats = run_dropin(amd, d)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
+    W = stats['W_rounds'][d['snap']]
+    for k in range(len(d['snap'])):
+        err = np.abs(W[k] - d['W'][k]).max()
+        assert err <= W_RTOL * np.abs(d['W'][k]).max(), (name, int(d['snap'][k]), err)
+    p = stats['p'].cpu().numpy()
+    assert np.abs(p - d['p'][-1]).max() <= P_RTOL * np.abs(d['p'][-1]).max()
+    np.testing.assert_allclose(tr.numpy(), d['train_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl.numpy(), d['test_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta.numpy() - d['test_acc']).max() <= acc_tol(d)
+    np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['rng_after'])
+
+
+@pytest.mark.parametrize('chunk', [1, 3, 7])
 @pytest.mark.parametrize('name', [c for c in LONG_CASES if 'fedamw' not in c])
-def test_dropin_shuffle_chunks(amd, monkeypatch, name, chunk):
-    """Shuffles generated K rounds per launch (FS_SHUFFLE_CHUNK; the default is 8) give
-    bitwise the same run as one launch per round, including a partial last chunk (R = 20),
-    and leave the generator where the reference leaves it."""
+def test_dropin_shuffle_chunks(amd, name, chunk):
+    """Shuffles generated K rounds per launch (options['shuffle_chunk']; the default is 8)
+    give bitwise the same run as one launch per round, including a partial last chunk (R =
+    20), and leave the generator where the reference leaves it."""
     d = load_long(name)
-    monkeypatch.setenv('FS_SHUFFLE_CHUNK', chunk)
-    (tr, tl, ta), st = run_dropin(amd, d)
+    (tr, tl, ta), st = run_dropin(amd, d, options={'shuffle_chunk': chunk})
     after = torch.empty(4, dtype=torch.int64).random_()
-    monkeypatch.setenv('FS_SHUFFLE_CHUNK', '8')
-    (tr8, tl8, ta8), st8 = run_dropin(amd, d)
+    (tr8, tl8, ta8), st8 = run_dropin(amd, d, options={'shuffle_chunk': 8})
     after8 = torch.empty(4, dtype=torch.int64).random_()
     assert np.array_equal(st['W_rounds'], st8['W_rounds'])
     assert torch.equal(tr, tr8) and torch.equal(tl, tl8) and torch.equal(ta, ta8) and torch.equal(after, after8)
 
 
+def _federation(amd, d, **kw):
+    Xs, ys = split_clients(d)
+    Xs = [torch.from_numpy(x) for x in Xs]
+    ys = [torch.from_numpy(y) for y in ys]
+    algo = str(d['algo'])
+    vl = _dl(d['X_val'], d['y_val']) if algo == 'fedamw' else None
+    lr_p = float(d['lr_p']) if algo == 'fedamw' else 1e-3
+    torch.manual_seed(int(d['torch_seed']))
+    return amd.tools.Federation(algo, Xs, ys, torch.from_numpy(d['X_test']), torch.from_numpy(d['y_test']), vl,
+                                *positional(d), lr_p, 'parallel' if str(d['mode']) == 'par' else 'sequential',
+                                verbose=False, **kw)
+
+
 @pytest.mark.parametrize('name', [c for c in LONG_CASES if 'seq' not in c])
-def test_dropin_deferred_eval(amd, monkeypatch, name):
+def test_dropin_deferred_eval(amd, name):
     """A round's evaluation carried by the next round's training launch (FS_PHASE_EVAL_DEFER, on
     the CUs the client groups leave idle) gives the same test loss / accuracy as a launch of its
-    own: the same per-row arithmetic, only the double-precision sum order of the partials
-    differs (rtol 1e-12); the training itself is bitwise unchanged."""
+    own: the same per-row arithmetic (eval_rows.h, shared by both), only the double-precision
+    sum order of the partials differs (rtol 1e-12); the training itself is bitwise unchanged."""
     d = load_long(name) if name in LONG_CASES else load(name)
-    monkeypatch.setenv('FS_EVAL_DEFER', '0')
-    (tr0, tl0, ta0), st0 = run_dropin(amd, d)
-    monkeypatch.setenv('FS_EVAL_DEFER', '1')
-    (tr1, tl1, ta1), st1 = run_dropin(amd, d)
+    if _federation(amd, d).plan.eval_blocks() == 0:
+        pytest.skip('the training launch of this shape carries no evaluation blocks')
+    (tr0, tl0, ta0), st0 = run_dropin(amd, d, options={'defer_eval': False})
+    (tr1, tl1, ta1), st1 = run_dropin(amd, d, options={'defer_eval': True})
     assert np.array_equal(st0['W_rounds'], st1['W_rounds']) and torch.equal(tr0, tr1)
     np.testing.assert_allclose(tl1.numpy(), tl0.numpy(), rtol=1e-12, atol=0)
     assert torch.equal(ta0, ta1)
 
 
-def test_deferred_eval_uses_idle_cus(amd, monkeypatch):
-    """A parallel split plan with fewer client groups than CUs carries evaluation blocks, and
-    a deferred evaluation lands in the history only once the next TRAIN (or any call
-    without one) has run; FS_EVAL_FUSE=0 turns the fusion off."""
+def test_deferred_eval_uses_idle_cus(amd):
+    """A parallel split plan with fewer client groups than CUs carries evaluation blocks (as
+    many as the CUs the groups leave idle, at most one per 16 test rows), and a deferred
+    evaluation lands in the history only once the next TRAIN (or any call without one) has
+    run; fs_tuning.no_eval_fuse turns the fusion off."""
     d = load_long([c for c in LONG_CASES if 'seq' not in c and 'fedamw' not in c][0])
-    monkeypatch.setenv('FS_EVAL_DEFER', '1')
     Xs, ys = split_clients(d)
     Xs = [torch.from_numpy(x) for x in Xs]
     ys = [torch.from_numpy(y) for y in ys]
@@ -132,7 +166,9 @@ def test_deferred_eval_uses_idle_cus(amd, monkeypatch):
     if fed.trainer.G < 2:
         pytest.skip('not a split launch at this shape')
     E = fed.plan.eval_blocks()
-    assert 0 < E <= 256 - fed.trainer.G
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    G, N = fed.trainer.G, len(ys)
+    assert E == min(cus - max(1, min(N, cus // G)) * G, (len(d['y_test']) + 15) // 16) and E > 0
     fed.eval_hist.fill_(-7.0)
     fed.round()                                    # evaluation of round 0 deferred
     torch.cuda.synchronize()
@@ -142,6 +178,8 @@ def test_deferred_eval_uses_idle_cus(amd, monkeypatch):
     assert float(fed.eval_hist[0, 0]) != -7.0 and float(fed.eval_hist[1, 0]) == -7.0
     tr, tl, ta = fed.results()                     # results() runs the pending one
     assert np.isfinite(tl[:2].numpy()).all() and float(fed.eval_hist[1, 0]) != -7.0
+    with amd.lib.tuning(no_eval_fuse=1):
+        assert _federation(amd, d).plan.eval_blocks() == 0
 
 
 def test_dropin_consumes_rng_like_reference(amd):
@@ -230,13 +268,10 @@ def test_local_train_vs_oracle(amd, D, C, B, sizes, prox, reg, mode):
 @pytest.mark.parametrize('G', [2, 4, 8, 16])
 @pytest.mark.parametrize('chained', [True, False])
 @pytest.mark.parametrize('prox', [True, False])
-@pytest.mark.parametrize('nw', [4, 8])
-def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
+def test_local_train_split_widths(amd, G, chained, prox):
     """Every group width of the split-client kernel, chained (one group walks the chain) and
-    parallel, 4-wave (two workgroups per CU) and 8-wave workgroups, against the oracle:
-    D = 1000 (16 tiles, the last one ragged), C = 10, tail batches of 1 and 7 rows, and a
-    client with no rows (its result is its start)."""
-    monkeypatch.setenv('FS_SPLIT_NW', str(nw))     # 4-wave workgroups are opt-in (the planner picks 8)
+    parallel, against the oracle: D = 1000 (16 tiles, the last one ragged), C = 10, tail
+    batches of 1 and 7 rows, and a client with no rows (its result is its start)."""
     rs = np.random.RandomState(G + 10 * chained + 100 * prox)
     D, C, B, E = 1000, 10, 32, 2
     sizes = [65, 33, 0, 7, 96, 40]
@@ -255,15 +290,13 @@ def test_local_train_split_widths(amd, monkeypatch, G, chained, prox, nw):
             start = Wr
 
 
-@pytest.mark.parametrize('sched', [0, 1, 2])
 @pytest.mark.parametrize('G,D', [(2, 2048), (4, 1000), (16, 4096)])
 @pytest.mark.parametrize('chained', [False, True])
-def test_local_train_split_schedules(amd, monkeypatch, sched, G, D, chained):
-    """Every hand-off / row-streaming schedule of the group kernel (FS_SP_SCHED; 2 is the
-    default: each wave's next rows are interleaved into its backward) against the oracle, with
-    full slices (16 tiles per workgroup: the straight-line interleaved backward) and ragged
-    ones (D = 1000), FedProx + ridge, chained and parallel."""
-    monkeypatch.setenv('FS_SP_SCHED', str(sched))
+def test_local_train_split_slices(amd, G, D, chained):
+    """The group kernel's row stream (each wave's next rows interleaved into its backward)
+    against the oracle, with full slices (16 tiles per workgroup: the straight-line
+    interleaved backward) and ragged ones (D = 1000), FedProx + ridge, chained and parallel."""
+    sched = 2
     rs = np.random.RandomState(sched + 10 * G + chained)
     C, B, E = 7, 32, 2
     sizes = [70, 0, 33, 64, 9]
@@ -300,21 +333,20 @@ def test_local_train_persistent_groups(amd, N, G):
         assert abs(loss[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
 
 
-def test_split_handoff_timeout_raises(amd, monkeypatch):
-    """A timed-out partner hand-off is reported, not silently absorbed: FS_SPIN_LIMIT=0 (the
-    test knob) makes the launch set its workspace error word; check_errors raises and clears
-    it, and the next launch is clean."""
+def test_split_handoff_timeout_raises(amd):
+    """A timed-out partner hand-off is reported, not silently absorbed: fs_tuning.inject_timeout
+    (the test knob) makes the launch set its workspace error word; check_errors raises and
+    clears it, and the next launch is clean."""
     rs = np.random.RandomState(1)
     Xs, ys = _rand_clients(rs, [40, 70], 256, 4)
     W0 = (rs.normal(size=(4, 256)) * 0.1).astype(np.float32)
-    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
-    with pytest.raises(amd.lib.FedsimError, match='timed out'):
-        _train_via_abi(amd, Xs, ys, W0, 0.3, 2, 32, False, 0.0, False, 0.0, False, seed=1, split=2)
-    monkeypatch.delenv('FS_SPIN_LIMIT')
+    with amd.lib.tuning(inject_timeout=1):
+        with pytest.raises(amd.lib.FedsimError, match='timed out'):
+            _train_via_abi(amd, Xs, ys, W0, 0.3, 2, 32, False, 0.0, False, 0.0, False, seed=1, split=2)
     _train_via_abi(amd, Xs, ys, W0, 0.3, 2, 32, False, 0.0, False, 0.0, False, seed=1, split=2)
 
 
-def test_mix_solve_timeout_raises(amd, monkeypatch):
+def test_mix_solve_timeout_raises(amd):
     """Same for the multi-CU p-solve, through the FedAMW drop-in: results() raises
     FedsimError instead of returning NaN mixture weights."""
     rs = np.random.RandomState(2)
@@ -323,8 +355,7 @@ def test_mix_solve_timeout_raises(amd, monkeypatch):
     Xv = (np.cos(rs.normal(size=(64, D))) / np.sqrt(D)).astype(np.float32)
     yv = rs.randint(0, C, size=64).astype(np.int64)
     T = torch.from_numpy
-    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
-    with pytest.raises(amd.lib.FedsimError, match='fs_mix_solve'):
+    with amd.lib.tuning(inject_timeout=1), pytest.raises(amd.lib.FedsimError, match='fs_mix_solve'):
         amd.tools.FedAMW([T(x) for x in Xs], [T(y) for y in ys], T(Xv), T(yv), _dl(Xv, yv), 'classification', C,
                          D, 0.5, 1, 32, False, 0.0, True, 1e-3, 1, 0.01, clients='parallel', verbose=False)
 
@@ -426,34 +457,29 @@ def test_mix_solve_auto_choice(amd, N, C, Bv, solver):
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
 
 
-@pytest.mark.parametrize('hops', [1, 2])
-@pytest.mark.parametrize('N,C,nv,Bv,S', [
-    (100, 10, 517, 16, None),   # config 2 shape: S = 8, K = 13 workgroups
-    (100, 10, 517, 16, 32),     # same, 4 workgroups of 32 clients
-    (1000, 10, 97, 16, None),   # config 5 client count: S = 32, K = 32
-    (300, 4, 60, 16, None),     # S = 16, ragged last slice
-    (129, 3, 77, 8, None),      # Bv < 16: idle rows, ragged last batch
-    (48, 16, 99, 16, 8),        # C = 16: every class slot real
-    (2000, 2, 45, 16, None),    # S = 64, K = 32
-    (5, 2, 40, 16, 8),          # one workgroup (K = 1)
-    (1100, 16, 40, 16, None),   # S = 64, C = 16
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (100, 10, 517, 16),     # config 2 shape: S = 8, K = 13 workgroups, one hop
+    (1000, 10, 97, 16),     # config 5 client count: S = 32, K = 32, two hops
+    (300, 4, 60, 16),       # S = 16, ragged last slice
+    (129, 3, 77, 8),        # Bv < 16: idle rows, ragged last batch (S = 16)
+    (48, 16, 99, 16),       # C = 16: every class slot real
+    (2000, 2, 45, 16),      # S = 64, K = 32
+    (5, 2, 40, 16),         # one workgroup (K = 1)
+    (1100, 16, 40, 16),     # S = 64, C = 16
 ])
-def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S, hops):
-    """fs_mix_solve's multi-CU solver (clients split over K workgroups, partial-logit exchange
-    every step: one hop, or reduce-scatter + all-gather) vs the oracle's p-SGD, 2 rounds x 2
-    epochs."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'mc')
-    monkeypatch.setenv('FS_MIX_MC_HOPS', str(hops))
-    if S:
-        monkeypatch.setenv('FS_MIX_MC_S', str(S))
+def test_mix_solve_multi_cu(amd, N, C, nv, Bv):
+    """fs_mix_solve's multi-CU solver (clients split over K workgroups of S, partial-logit
+    exchange every step: one hop at S = 8, reduce-scatter + all-gather above) vs the oracle's
+    p-SGD, 2 rounds x 2 epochs."""
     # (at N >= 1000, lr_p = 0.5 drives p to |p| ~ 10 within a few steps, where any two fp32
     # summation orders of the 10^4-term logits drift past 1e-5; the configs use lr_p ~ 1e-3)
-    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)
+    with amd.lib.tuning(mix_solver='mc'):
+        test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)
     mode = amd.lib.lib().fs_mix_solve_last_mode()
     assert mode == 2, mode             # the multi-CU solver ran (a timed-out spin raises in check_errors)
 
 
-@pytest.mark.parametrize('h', ['0', '16'])
+@pytest.mark.parametrize('h', [-1, 16])
 @pytest.mark.parametrize('N,C,nv,Bv', [
     (1000, 10, 97, 16),     # config 5 client count: K = 8 workgroups of 128 clients
     (300, 4, 60, 16),       # K = 3, ragged last slice
@@ -462,39 +488,21 @@ def test_mix_solve_multi_cu(amd, monkeypatch, N, C, nv, Bv, S, hops):
     (1000, 16, 40, 16),     # C = 16: 64 clients per workgroup, K = 16
     (200, 10, 133, 16),     # K = 2
 ])
-def test_mix_solve_qmc(amd, monkeypatch, N, C, nv, Bv, h):
+def test_mix_solve_qmc(amd, N, C, nv, Bv, h):
     """fs_mix_solve's multi-CU quarter-wave solver (clients over K workgroups, one exchange of
-    the partial logits per step; with / without L2 prefetch helpers) vs the oracle's p-SGD."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'qmc')
-    monkeypatch.setenv('FS_MIX_PF_H', h)
-    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
+    the partial logits per step; without / with L2 prefetch helpers) vs the oracle's p-SGD."""
+    with amd.lib.tuning(mix_solver='qmc', mix_prefetch=h):
+        test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
 
 
-def test_mix_solve_qmc_timeout_raises(amd, monkeypatch):
-    """A timed-out exchange of the multi-CU quarter-wave solver sets the error word."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'qmc')
-    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
-    with pytest.raises(amd.lib.FedsimError):
+def test_mix_solve_qmc_timeout_raises(amd):
+    """A timed-out exchange of the multi-CU quarter-wave solver sets the error word; the next
+    solve is clean."""
+    with amd.lib.tuning(mix_solver='qmc'):
+        with amd.lib.tuning(inject_timeout=1), pytest.raises(amd.lib.FedsimError):
+            test_mix_solve_variants(amd, 300, 4, 60, 16)
         test_mix_solve_variants(amd, 300, 4, 60, 16)
-
-
-@pytest.mark.parametrize('rw', [1, 2, 4, 8])
-@pytest.mark.parametrize('N,C,nv,Bv', [
-    (100, 10, 517, 16),     # config 2 shape: NK = 2, CP = 16
-    (10, 2, 203, 16),       # config 1 shape: NK = 1, CP = 2
-    (200, 4, 301, 16),      # NK = 4
-    (129, 3, 77, 8),        # Bv < 16: fewer workgroups, ragged last batch
-    (5, 3, 40, 7),          # Bv = 7: the last workgroup's rows partly idle
-    (37, 16, 90, 16),       # C = 16: every class slot real
-])
-def test_mix_solve_rows(amd, monkeypatch, N, C, nv, Bv, rw):
-    """fs_mix_solve's row-split solver (batch rows over K = Bv / rw workgroups, one exchange of
-    the N partial gradients per step) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'rows')
-    monkeypatch.setenv('FS_MIX_ROWS_RW', str(rw))
-    test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.1 if N == 200 else 0.5)
-    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'rows'
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [
@@ -509,33 +517,20 @@ def test_mix_solve_rows(amd, monkeypatch, N, C, nv, Bv, rw):
     (128, 10, 77, 8),       # N = 128 (NK = 8 exactly), Bv = 8
     (65, 9, 211, 16),       # NK = 8, C = 9 < CL = 10 (class padding), ragged chunks
 ])
-def test_mix_solve_quad(amd, monkeypatch, N, C, nv, Bv):
+def test_mix_solve_quad(amd, N, C, nv, Bv):
     """fs_mix_solve's quarter-wave solver (4 batch rows per wave, 16 lanes per row; default
     issue split and L2 prefetch helpers) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
-    test_mix_solve_variants(amd, N, C, nv, Bv)
+    with amd.lib.tuning(mix_solver='quad'):
+        test_mix_solve_variants(amd, N, C, nv, Bv)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [(100, 10, 517, 16), (60, 8, 33, 9), (37, 16, 90, 16)])
-def test_mix_solve_quad_libm_softmax(amd, monkeypatch, N, C, nv, Bv):
+def test_mix_solve_quad_libm_softmax(amd, N, C, nv, Bv):
     """The quarter-wave solver with torch's softmax form on libm expf / logf
-    (FS_MIX_QUAD_FASTEXP=0; the default is v_exp / v_rcp) vs the oracle."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
-    monkeypatch.setenv('FS_MIX_QUAD_FASTEXP', '0')
-    test_mix_solve_variants(amd, N, C, nv, Bv)
-    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
-
-
-@pytest.mark.parametrize('split', [5, 7, 10])
-@pytest.mark.parametrize('oob', [0, 1])
-def test_mix_solve_quad_issue_forms(amd, monkeypatch, split, oob):
-    """The quarter-wave solver's other load-issue splits (classes issued at the end of a step,
-    the rest after the next step's logits) and padding-chunk forms at config 2's shape."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'quad')
-    monkeypatch.setenv('FS_MIX_QUAD_SPLIT', str(split))
-    monkeypatch.setenv('FS_MIX_QUAD_OOB', str(oob))
-    test_mix_solve_variants(amd, 100, 10, 517, 16)
+    (fs_tuning.mix_exact_softmax; the default is v_exp / v_rcp) vs the oracle."""
+    with amd.lib.tuning(mix_solver='quad', mix_exact_softmax=1):
+        test_mix_solve_variants(amd, N, C, nv, Bv)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
 
 
@@ -546,13 +541,12 @@ def test_mix_solve_quad_issue_forms(amd, monkeypatch, split, oob):
     (129, 3, 77, 8),        # NK = 4, Bv < 16: idle waves in the helpers too, ragged last batch
 ])
 @pytest.mark.parametrize('solver', ['reg', 'quad'])
-def test_mix_solve_prefetch_helpers(amd, monkeypatch, N, C, nv, Bv, h, lead, solver):
-    """The single-CU solvers with L2 prefetch helper workgroups (FS_MIX_PF_H): the helpers
-    only load, so p and the momentum buffer are bitwise those of the solver alone, and match
-    the oracle's p-SGD."""
+def test_mix_solve_prefetch_helpers(amd, N, C, nv, Bv, h, lead, solver):
+    """The single-CU solvers with L2 prefetch helper workgroups (fs_tuning.mix_prefetch): the
+    helpers only load, so p and the momentum buffer are bitwise those of the solver alone, and
+    match the oracle's p-SGD."""
     if solver == 'quad' and N > 128:
         pytest.skip('the quarter-wave solver covers N <= 128')
-    monkeypatch.setenv('FS_MIX_SOLVER', solver)
     rs = np.random.RandomState(N + nv)
     D = 64
     Xv = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
@@ -561,46 +555,30 @@ def test_mix_solve_prefetch_helpers(amd, monkeypatch, N, C, nv, Bv, h, lead, sol
     Ws = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.5).astype(np.float32))
     dev = torch.device('cuda')
     out = []
-    for helpers in (0, h):
-        monkeypatch.setenv('FS_MIX_PF_H', str(helpers))
-        monkeypatch.setenv('FS_MIX_PF_LEAD', str(lead))
-        mix = amd.engine.Mixture(Xv, yv, D, C, N, Bv, p0, dev)
-        Wd = torch.zeros(N, C, mix.f.ld, device=dev)
-        Wd[:, :, :D] = Ws
-        for rnd in range(2):
-            torch.manual_seed(90 + rnd)
-            mix.solve(Wd, amd.rng.draw_pass_seeds(3), 0.5)
-        torch.cuda.synchronize()
-        mix.check_errors()
+    for helpers in (-1, h):
+        with amd.lib.tuning(mix_solver=solver, mix_prefetch=helpers, mix_prefetch_lead=lead):
+            mix = amd.engine.Mixture(Xv, yv, D, C, N, Bv, p0, dev)
+            Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+            Wd[:, :, :D] = Ws
+            for rnd in range(2):
+                torch.manual_seed(90 + rnd)
+                mix.solve(Wd, amd.rng.draw_pass_seeds(3), 0.5)
+            torch.cuda.synchronize()
+            mix.check_errors()
         assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
         out.append((mix.p.cpu().clone(), mix.buf.cpu().clone()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
-    monkeypatch.setenv('FS_MIX_PF_H', str(h))
-    test_mix_solve_variants(amd, N, C, nv, Bv)
-
-
-def test_mix_solve_rows_timeout_raises(amd, monkeypatch):
-    """A timed-out exchange of the row-split solver sets the error word: check_errors raises."""
-    monkeypatch.setenv('FS_MIX_SOLVER', 'rows')
-    monkeypatch.setenv('FS_SPIN_LIMIT', '0')
-    with pytest.raises(amd.lib.FedsimError):
-        test_mix_solve_variants(amd, 100, 10, 64, 16)
-    monkeypatch.delenv('FS_SPIN_LIMIT')
-    test_mix_solve_variants(amd, 100, 10, 64, 16)
+    with amd.lib.tuning(mix_solver=solver, mix_prefetch=h):
+        test_mix_solve_variants(amd, N, C, nv, Bv)
 
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
                                         ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('wave', 10, 2),
-                                        ('reg2-select', 100, 10),
-                                        ('reg2-select', 129, 3)])
-def test_mix_solve_forced_fallbacks(amd, monkeypatch, solver, N, C):
-    """The solvers the auto choice does not take at these shapes (reg2-select: form 2 with the
-    select-form reduce-scatter instead of the permlane swap-add levels)."""
-    if solver == 'reg2-select':
-        monkeypatch.setenv('FS_MIX_SWAP', '0')
-        solver = 'reg2'
-    monkeypatch.setenv('FS_MIX_SOLVER', solver)
-    test_mix_solve_variants(amd, N, C, 133, 16, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
+                                        ('reg2', 100, 10)])
+def test_mix_solve_forced_fallbacks(amd, solver, N, C):
+    """The solvers the auto choice does not take at these shapes, forced through fs_tuning."""
+    with amd.lib.tuning(mix_solver=solver):
+        test_mix_solve_variants(amd, N, C, 133, 16, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
 
 

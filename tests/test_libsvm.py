@@ -115,3 +115,33 @@ def test_load_full_data_uses_the_file(tmp_path):
     assert np.array_equal(ytr, utils.svmlight_labels(ys, 'toy'))
     assert np.array_equal(yte, utils.svmlight_labels(yts, 'toy'))
     assert d == Xs.shape[1] and C == 3 and sum(len(p) for p in parts) == 300
+
+
+def test_unsorted_or_duplicate_indices_rejected(tmp_path):
+    """load_svmlight_file raises ValueError when a line's indices are not strictly increasing;
+    the native reader refuses the same files (it used to keep the last value)."""
+    for name, text in (('uns', '1 1:1 3:2 2:5\n'), ('dup', '0 2:1\n1 1:1 1:2\n')):
+        p = str(tmp_path / name)
+        with open(p, 'w') as f:
+            f.write(text)
+        with pytest.raises(ValueError, match='sorted and unique'):
+            load_svmlight_file(p)
+        with pytest.raises(_lib.FedsimError, match='sorted and unique'):
+            utils.read_libsvm(p)
+
+
+def test_load_full_data_index_base_per_file(tmp_path):
+    """The reference calls load_svmlight_file once per file, each with zero_based='auto':
+    a training file that uses feature 0 and a test file that does not are read with
+    different bases (the test file at the training width)."""
+    with open(tmp_path / 'mix', 'w') as f:
+        f.write(''.join('%d 0:1 %d:2\n' % (i % 2, 1 + i % 5) for i in range(40)))
+    with open(tmp_path / 'mix.t', 'w') as f:
+        f.write(''.join('%d %d:3 6:1\n' % (i % 2, 1 + i % 4) for i in range(12)))
+    Xtr, ytr, Xte, yte, parts, d, C = utils.load_full_data('mix', 2, 0.5, root_dir=str(tmp_path) + '/',
+                                                           verbose=False)
+    Xs, _ = _sk(str(tmp_path / 'mix'))
+    Xts, _ = _sk(str(tmp_path / 'mix.t'), n_features=Xs.shape[1])
+    assert d == Xs.shape[1] == 6
+    assert np.array_equal(Xtr, Xs) and np.array_equal(Xte, Xts)
+    assert Xte[0, 0] == 3.0 and Xte[0, 5] == 1.0      # one-based: index 1 -> column 0

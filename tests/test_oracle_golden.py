@@ -4,8 +4,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol, load,
-                            load_long, positional, split_clients)
+from tests.fixtures import (BENCH_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol,
+                            load, load_bench, load_long, positional, split_clients)
 
 
 def run_oracle(d):
@@ -83,3 +83,20 @@ def test_long_horizon_matches_reference(name):
     assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)
     if 'p' in d:
         assert np.abs(trace['p'] - d['p']).max() <= P_RTOL * np.abs(d['p']).max()
+
+
+@pytest.mark.parametrize('name', BENCH_CASES)
+def test_benchmark_length_fedamw_matches_reference(name):
+    """FedAMW at config 2's N = 100, C = 10 with n_v >= 2,000 and R = 34 rounds: >= 5,000
+    dependent p-SGD steps per round, ~180,000 in all -- the fp32 drift of the p-solve at
+    benchmark length, pinned to the reference (p after every round, W at the snapshot rounds)."""
+    d = load_bench(name)
+    assert int(d['R']) * ((int(d['n_val']) + 15) // 16) >= 5000
+    tr, tl, ta, trace = run_oracle(d)
+    for k, t in enumerate(d['snap']):
+        assert np.abs(trace['W'][t] - d['W'][k]).max() <= W_RTOL * np.abs(d['W'][k]).max(), (name, t)
+    for t in range(len(d['p'])):
+        assert np.abs(trace['p'][t] - d['p'][t]).max() <= P_RTOL * np.abs(d['p'][t]).max(), (name, t)
+    np.testing.assert_allclose(tr, d['train_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl, d['test_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)

@@ -7,6 +7,8 @@ product's host-side partitioner (functions/utils.get_Dirichlet_distribution) aga
 fixtures.  Tolerances: indices, labels, splits and RNG states exact; features 1e-5 absolute
 (numpy's float32 cos vs torch's; |phi| <= 1/sqrt(D)); heterogeneity 1e-4 relative (a
 difference of near-equal fp32 Gram matrices; the reference reduces in torch's order)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -64,3 +66,39 @@ def test_exp_prepare_matches_reference():
         assert abs(float(r['X_clients'][j].astype(np.float64).sum()) - d['phi_sum'][j]) <= 1e-5 * r['X_clients'][j].size
     assert abs(r['hete'] - float(d['hete'])) <= 1e-4 * abs(float(d['hete']))
     assert np.abs(r['X_test'][:16] - d['phi_test_head']).max() <= 1e-5
+
+
+def test_oracle_exp_sequence_matches_reference():
+    """exp.py's whole sequence on one un-reseeded stream (exp_satimage.npz): the oracle's
+    restatement of exp.py:60-99 and its six algorithms called in exp.py's order, against
+    every value the reference returned, the heterogeneity and both generators' end state."""
+    import json
+    from tests.fixtures import GOLDEN, LOSS_RTOL
+    d = load('exp_satimage')
+    P = json.load(open(os.path.join(GOLDEN, 'params.json')))[str(d['dataset'])]
+    y, yt = d['y'] - d['y'].min(), d['y_test'] - d['y'].min()         # utils.py:43-44 (> 2 classes)
+    D, N, R, le, B = int(d['D']), int(d['N']), int(d['Round']), int(d['local_epoch']), int(d['batch_size'])
+    C = int(d['C'])
+    torch.manual_seed(100)
+    np.random.seed(100)
+    r = O.exp_prepare(d['X'], y, d['X_test'], yt, N, float(d['alpha']), P['kernel_par'], D)
+    a = (r['X_train'], r['y_train'], r['X_test'], yt.astype(np.int64))
+    lr = P['lr']
+    out = [O.Centralized(*a, 'classification', C, D, lr, le * R, B, False, 0, False, 0),
+           O.Distributed(*a, 'classification', C, D, lr, le * R, B, False, 0, False, 0),
+           O.FedAMW_OneShot(*a, r['X_val'], r['y_val'], 'classification', C, D, lr, le * R, B, False, 0, True,
+                            P['lambda_reg_os'], R, P['lr_p_os']),
+           O.FedAvg(*a, 'classification', C, D, lr, le, B, False, 0, False, 0, R),
+           O.FedProx(*a, 'classification', C, D, lr, le, B, True, P['lambda_prox'], False, 0, R),
+           O.FedAMW(*a, r['X_val'], r['y_val'], 'classification', C, D, lr, le, B, False, 0, True, P['lambda_reg'], R,
+                    P['lr_p'])]
+    np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['after_torch'])
+    np.testing.assert_array_equal(np.random.randint(0, 1 << 30, 4), d['after_np'])
+    assert abs(r['hete'] - float(d['heterogeneity'])) <= 1e-4 * abs(float(d['heterogeneity']))
+    for k, o in enumerate(out):
+        for j, key in enumerate(('train_loss', 'test_loss')):
+            got = np.broadcast_to(np.asarray(o[j], dtype=np.float64), (R,))
+            np.testing.assert_allclose(got, d[key][k], rtol=0, atol=LOSS_RTOL * max(1.0, np.abs(d[key][k]).max()),
+                                       err_msg='%s %d' % (key, k))
+        acc = np.broadcast_to(np.asarray(o[2], dtype=np.float64), (R,))
+        assert np.abs(acc - d['test_acc'][k]).max() <= 100.0 / len(yt) + 1e-4, k
