@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 9
+#define FS_ABI_VERSION 10
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -66,6 +66,9 @@ const char* fs_last_error(void);
  *   spin_limit         bound of every cross-workgroup spin, in polls (0 = the default)
  *   inject_timeout     test knob: 1 = every exchanging launch reports a timeout at its first
  *                      hand-off (the error path without a real hang)
+ *   train_form         (ABI 10) fs_local_train_plan's choice for parallel clients: 0 = by shape
+ *                      (the pair form where it fits, else the split form), 1 = never the pair
+ *                      form, 2 = the pair form wherever it fits (else as 0)
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -85,6 +88,7 @@ typedef struct fs_tuning {
   int no_eval_fuse;
   unsigned spin_limit;
   int inject_timeout;
+  int train_form;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -153,11 +157,19 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              the clients (LPT order, snake over the groups); chained clients: one
  *              group walks the chain with the weights kept in registers.  The error
  *              word (last 256 bytes of d_ws) is nonzero after the kernel if a partner
- *              never arrived (results invalid).  fs_local_train_plan: *G_out on entry is
- *              a request (0 = planner's choice, 1 = one workgroup per client, 2..16 = that
- *              width if the shape allows it); prox says whether the FedProx term is on.
+ *              never arrived (results invalid).
+ *              G | FS_G_PAIR (ABI 10, parallel clients, ld == 512 G): the "pair" form --
+ *              min(ceil(N/2), CUs/G) groups of G workgroups, each training TWO clients at a
+ *              time interleaved, so one client's hand-off overlaps the other's compute and
+ *              the feature rows stream through every phase; the same arithmetic as the split
+ *              form at width G (bitwise the same results).
+ *              fs_local_train_plan: *G_out on entry is a request (0 = planner's choice, 1 =
+ *              one workgroup per client, 2..16 = that split width if the shape allows it,
+ *              G | FS_G_PAIR = the pair form at that width if the shape allows it); prox says
+ *              whether the FedProx term is on.
  * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
  * ------------------------------------------------------------------------- */
+#define FS_G_PAIR 256
 int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                         int* G_out, int64_t* ws_bytes_out);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,

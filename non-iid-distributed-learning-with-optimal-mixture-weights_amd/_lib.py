@@ -62,9 +62,10 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
+G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
 SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc'}
 SOLVERS = {v: k for k, v in SOLVER_NAMES.items() if k}
@@ -74,7 +75,7 @@ class Tuning(C.Structure):
     """fs_tuning (include/fedsim.h), field for field: how -- never what -- the kernels compute."""
     _fields_ = [('mix_solver', C.c_int), ('mix_prefetch', C.c_int), ('mix_prefetch_lead', C.c_int),
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
-                ('inject_timeout', C.c_int)]
+                ('inject_timeout', C.c_int), ('train_form', C.c_int)]
 
 
 class PlanDesc(C.Structure):

@@ -47,6 +47,8 @@ extern "C" int64_t fs_tuning_size(void) { return (int64_t)sizeof(fs_tuning); }
 extern "C" int fs_set_tuning(const fs_tuning* t) {
   if (t && (t->mix_prefetch < -1 || t->mix_prefetch > 224 || t->mix_prefetch_lead < 0))
     return fs::fail(FS_EINVAL, "fs_set_tuning: mix_prefetch must be in [-1, 224], mix_prefetch_lead >= 0");
+  if (t && (t->train_form < 0 || t->train_form > 2))
+    return fs::fail(FS_EINVAL, "fs_set_tuning: train_form must be 0, 1 or 2");
   std::lock_guard<std::mutex> lk(fs::g_tune_m);
   fs::g_tune = t ? *t : fs_tuning{};
   return FS_OK;

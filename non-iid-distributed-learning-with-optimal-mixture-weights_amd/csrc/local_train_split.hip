@@ -38,6 +38,7 @@
 #include "common.h"
 #include "eval_rows.h"
 #include "lanes.h"
+#include "split_common.h"
 
 namespace fs {
 
@@ -62,63 +63,6 @@ constexpr int SP_ERR_BYTES = 256;         // error block at the END of the works
 #else
 #define SP_STAMP(k)
 #endif
-
-struct SplitWS {
-  unsigned* err;                       // [1] sticky; nonzero: a partner never arrived (spin bound hit)
-  unsigned long long* xbuf;            // [ngroups][2][G][SZ] published partials: {tag, value} granules
-  unsigned long long* stamps;          // [grid][16] diagnostic build only
-  int SZ;                              // granules per (group, parity, slice)
-  unsigned tag_base;                   // launch generation << 20 (0: the buffer was zeroed for this launch)
-  int ngroups;
-  unsigned spin_limit;                 // 0: test knob -- report a timeout at the first hand-off
-};
-
-__device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
-
-// LDS image of one step's batch slice: row-major, row stride RS = DS + 8 floats, and the
-// sixteen float4 blocks of every 64-column tile permuted by block ^ (row & 7).  With this
-// layout both the image write (lanes 0-7 = eight rows, same block) and the backward's read
-// (lanes = 16 blocks of one row, 4 rows per instruction) are bank-conflict free.
-__device__ __forceinline__ int img_off(int row, int RS, int tile, int blk) {
-  return row * RS + 64 * tile + 4 * (blk ^ (row & 7));
-}
-
-// Client k of a group's sequence (-1: none).  Parallel: tier k of the LPT-ordered clients,
-// snake order (even tiers forward, odd tiers backward) so the groups' step totals balance.
-__device__ __forceinline__ int sp_client(const LTParams& P, int grp, int ng, int k) {
-  if (P.chained) return k < P.N ? k : -1;
-  const int idx = k * ng + ((k & 1) ? ng - 1 - grp : grp);
-  if (idx >= P.N) return -1;
-  return P.order ? P.order[idx] : idx;
-}
-
-// A position in the group's step sequence: client (k, j), step st of its E * nbat steps.
-struct SpCur {
-  int k, j, n, nbat, steps, st;
-  int64_t row0;
-};
-
-// first client with at least one step at sequence position >= k (false: sequence exhausted)
-__device__ __forceinline__ bool sp_seek(SpCur& c, const LTParams& P, int grp, int ng, int T, int k) {
-  for (; k < T; ++k) {
-    const int j = sp_client(P, grp, ng, k);
-    if (j < 0) continue;
-    const int64_t r0 = P.row_off[j];
-    const int n = (int)(P.row_off[j + 1] - r0);
-    const int nbat = (n + P.B - 1) / P.B;
-    if (nbat == 0 || P.E == 0) continue;
-    c.k = k; c.j = j; c.n = n; c.nbat = nbat; c.steps = P.E * nbat; c.st = 0; c.row0 = r0;
-    return true;
-  }
-  c.k = T;
-  return false;
-}
-
-__device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp, int ng, int T) {
-  if (c.k >= T) return false;
-  if (++c.st < c.steps) return true;
-  return sp_seek(c, P, grp, ng, T, c.k + 1);
-}
 
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
@@ -596,9 +540,20 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #endif
 }
 
+unsigned exchange_generation(const void* ws, bool long_launch) {
+  static std::mutex gm;
+  static std::unordered_map<const void*, unsigned> gens;
+  std::lock_guard<std::mutex> lk(gm);
+  auto it = gens.find(ws);
+  const unsigned prev = it == gens.end() ? 0u : it->second;
+  const unsigned gen = (long_launch || prev >= 4095u) ? 0u : prev + 1u;
+  gens[ws] = gen;
+  return gen;
+}
+
 static int g_cus = 0;
 
-static int device_cus() {
+int device_cus() {
   if (g_cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -695,19 +650,10 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   // when a workspace is first seen, every 4095 launches (the generation wraps) and for a
   // launch whose groups may run 2^20 - 1 steps or more (then the generation is 0: tags are
   // the step + 1 alone, as after any clearing).
-  unsigned gen = 0;
-  {
-    static std::mutex gm;
-    static std::unordered_map<const void*, unsigned> gens;
-    // (groups walk clients in snake order: at most ceil(N / ng) each; chained: all N)
-    const int64_t groups_clients = P.chained ? P.N : (P.N + ng - 1) / ng;
-    const bool long_launch = P.max_client_steps <= 0 || P.max_client_steps * groups_clients >= (1 << 20) - 1;
-    std::lock_guard<std::mutex> lk(gm);
-    auto it = gens.find(ws);
-    const unsigned prev = it == gens.end() ? 0u : it->second;
-    gen = (long_launch || prev >= 4095u) ? 0u : prev + 1u;
-    gens[ws] = gen;
-  }
+  // (groups walk clients in snake order: at most ceil(N / ng) each; chained: all N)
+  const int64_t groups_clients = P.chained ? P.N : (P.N + ng - 1) / ng;
+  const bool long_launch = P.max_client_steps <= 0 || P.max_client_steps * groups_clients >= (1 << 20) - 1;
+  const unsigned gen = exchange_generation(ws, long_launch);
   X.tag_base = gen << 20;
   if (gen <= 1) {                      // first use, wrap or long launch: clear the granules
     hipError_t e = hipMemsetAsync(base, 0, (size_t)xbytes, st);
@@ -727,6 +673,12 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
 
 int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained) {
   const int NT = (int)(ld >> 6);
+  if (G & FS_G_PAIR) {
+    const int g = G & (FS_G_PAIR - 1);
+    const int cus = device_cus();
+    if (chained || cus <= 0 || !pair_fits(C, B, NT, g)) return 0;
+    return std::max(0, cus - pair_groups(N, g, cus) * g);
+  }
   if (chained || G < 2 || C > 16 || B > 32 || !split_fits(C, B, NT, G)) return 0;
   const int cus = device_cus();
   if (cus <= 0) return 0;
@@ -754,7 +706,16 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   const int cus = device_cus();
   if (want == 1 || C > 16 || B > 32 || cus <= 0) return FS_OK;
   const int NT = (int)(ld >> 6);
-  int G = (want > 1 && split_fits(C, B, NT, want) && want <= cus) ? want : 0;
+  // an explicit pair request
+  if (want & FS_G_PAIR) {
+    const int g = want & (FS_G_PAIR - 1);
+    if (!chained && pair_fits(C, B, NT, g) && g <= cus) {
+      *G_out = g | FS_G_PAIR;
+      *ws_bytes_out = pair_ws_bytes(N, g, B, cus);
+      return FS_OK;
+    }
+  }
+  int G = (want > 1 && want < FS_G_PAIR && split_fits(C, B, NT, want) && want <= cus) ? want : 0;
   if (G == 0) {
     if (chained) {
       // one group walks the chain: slice one step's batch (B x ld floats) to ~32 KB per CU
@@ -765,12 +726,25 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
           if (bytes / cand <= 32 * 1024) break;
         }
     } else {
-      // parallel clients: the narrowest group that fits (most clients in flight, fewest
+      // parallel clients: the narrowest split group that fits (most clients in flight, fewest
       // partners) -- FedProx too since its anchor is re-read, not register-resident (r02t, prox,
       // us per launch, G = 1 vs split: config 2 741 / 362, config 3 5955 / 5263, config 4
       // 580 / 508, config 5 11237 / 7003)
       for (int cand : {2, 4, 8, 16})
         if (split_fits(C, B, NT, cand) && cand <= cus) { G = cand; break; }
+      // ... unless the pair form fits and its groups would walk several clients each (where it
+      // measured faster: config 3 5.16 vs 5.26 ms, config 4 0.434 vs 0.457 ms; with one client
+      // per group, config 2, the split form: 0.343 vs 0.366 ms -- profiles/r03/pair_ab.txt), or
+      // fs_tuning.train_form asks for it (1: never, 2: wherever it fits)
+      const int form = tuning().train_form;
+      if (form != 1)
+        for (int cand : {2, 4, 8, 16})
+          if (pair_fits(C, B, NT, cand) && cand <= cus &&
+              (form == 2 || G == 0 || (int64_t)N > (int64_t)split_groups(N, G, 0, cus))) {
+            *G_out = cand | FS_G_PAIR;
+            *ws_bytes_out = pair_ws_bytes(N, cand, B, cus);
+            return FS_OK;
+          }
       (void)prox;
     }
   }

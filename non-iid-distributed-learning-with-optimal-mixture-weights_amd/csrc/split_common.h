@@ -1,0 +1,101 @@
+// Pieces shared by the split-client (local_train_split.hip) and pair-client
+// (local_train_pair.hip) local-training kernels: the exchange workspace, the LDS image
+// layout of one step's batch slice, and the walk of a group's client sequence.
+#pragma once
+
+#include "common.h"
+
+namespace fs {
+
+int device_cus();   // CUs of the current device (cached)
+
+// Hand-off tags of an exchanging launch: (launch generation << 20) + step + 1, the generation
+// counted per workspace on the host, so a granule left by an earlier launch never carries a
+// tag this launch waits for and the exchange buffer needs no clearing per launch.  0 (the
+// caller then clears the granules): a workspace's first use, every 4095 launches (the
+// generation wraps), and a launch whose client sequences may run 2^20 - 1 steps or more.
+unsigned exchange_generation(const void* ws, bool long_launch);
+
+// the pair form (local_train_pair.hip)
+bool pair_fits(int C, int B, int NT, int G);
+int pair_groups(int N, int G, int cus);
+int64_t pair_ws_bytes(int N, int G, int B, int cus);
+
+struct SplitWS {
+  unsigned* err;                       // [1] sticky; nonzero: a partner never arrived (spin bound hit)
+  unsigned long long* xbuf;            // [ngroups][2][G][SZ] published partials: {tag, value} granules
+  unsigned long long* stamps;          // [grid][16] diagnostic build only
+  int SZ;                              // granules per (group, parity, slice)
+  unsigned tag_base;                   // launch generation << 20 (0: the buffer was zeroed for this launch)
+  int ngroups;
+  unsigned spin_limit;                 // 0: test knob -- report a timeout at the first hand-off
+};
+
+__device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
+
+// LDS image of one step's batch slice: row-major, row stride RS = DS + 8 floats, and the
+// sixteen float4 blocks of every 64-column tile permuted by block ^ (row & 7).  With this
+// layout both the image write (lanes 0-7 = eight rows, same block) and the backward's read
+// (lanes = 16 blocks of one row, 4 rows per instruction) are bank-conflict free.
+__device__ __forceinline__ int img_off(int row, int RS, int tile, int blk) {
+  return row * RS + 64 * tile + 4 * (blk ^ (row & 7));
+}
+
+// Reads of the read-only client tables (row_off, order).  SC = true: scalar loads
+// (lgkmcnt), so that a client boundary never waits for the vector-memory queue -- where
+// the pair kernel keeps a step's row stream in flight; false: ordinary loads.
+__device__ __forceinline__ int tab_i32(const int32_t* base, int i) {
+  const int32_t* p = base + __builtin_amdgcn_readfirstlane(i);
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ int64_t tab_i64(const int64_t* base, int i) {
+  const int64_t* p = base + __builtin_amdgcn_readfirstlane(i);
+  int64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+
+// Client k of a group's sequence (-1: none).  Parallel: tier k of the LPT-ordered clients,
+// snake order (even tiers forward, odd tiers backward) so the groups' step totals balance.
+template <bool SC = false>
+__device__ __forceinline__ int sp_client(const LTParams& P, int grp, int ng, int k) {
+  if (P.chained) return k < P.N ? k : -1;
+  const int idx = k * ng + ((k & 1) ? ng - 1 - grp : grp);
+  if (idx >= P.N) return -1;
+  if (!P.order) return idx;
+  return SC ? tab_i32(P.order, idx) : P.order[idx];
+}
+
+// A position in the group's step sequence: client (k, j), step st of its E * nbat steps.
+struct SpCur {
+  int k, j, n, nbat, steps, st;
+  int64_t row0;
+};
+
+// first client with at least one step at sequence position >= k (false: sequence exhausted)
+template <bool SC = false>
+__device__ __forceinline__ bool sp_seek(SpCur& c, const LTParams& P, int grp, int ng, int T, int k) {
+  for (; k < T; ++k) {
+    const int j = sp_client<SC>(P, grp, ng, k);
+    if (j < 0) continue;
+    const int64_t r0 = SC ? tab_i64(P.row_off, j) : P.row_off[j];
+    const int n = (int)((SC ? tab_i64(P.row_off, j + 1) : P.row_off[j + 1]) - r0);
+    const int nbat = (n + P.B - 1) / P.B;
+    if (nbat == 0 || P.E == 0) continue;
+    c.k = k; c.j = j; c.n = n; c.nbat = nbat; c.steps = P.E * nbat; c.st = 0; c.row0 = r0;
+    return true;
+  }
+  c.k = T;
+  return false;
+}
+
+template <bool SC = false>
+__device__ __forceinline__ bool sp_advance(SpCur& c, const LTParams& P, int grp, int ng, int T) {
+  if (c.k >= T) return false;
+  if (++c.st < c.steps) return true;
+  return sp_seek<SC>(c, P, grp, ng, T, c.k + 1);
+}
+
+}  // namespace fs

@@ -134,8 +134,9 @@ class LocalTrainer:
 
     ``split``: workgroups per client.  None asks fs_local_train_plan (a group of G
     workgroups splits each client's feature dimension whenever the shape allows, in parallel
-    mode as persistent groups over the clients, in chained mode as one group walking the
-    chain); 1 forces one workgroup per client."""
+    mode as persistent groups over the clients -- two clients per group in the pair form
+    (G | _lib.G_PAIR) where the shape allows it -- in chained mode as one group walking the
+    chain); 1 forces one workgroup per client, G a split width, G | _lib.G_PAIR the pair form."""
 
     def __init__(self, feats, C, B, E, split=None, chained=False, rows=None, prox=False):
         self.f = feats
@@ -165,9 +166,20 @@ class LocalTrainer:
         if split is not None and int(split) != g.value:
             raise _lib.FedsimError('fs_local_train_plan: G=%d is not available for this shape (planner: %d)'
                                    % (int(split), g.value))
-        self.G = int(g.value)
+        self.G = int(g.value)                       # as the ABI takes it (G | G_PAIR: the pair form)
+        self.pair = bool(self.G & _lib.G_PAIR)
+        self.width = self.G & (_lib.G_PAIR - 1)     # workgroups per client group
         self.ws = (torch.zeros(max(2 * _lib.ERR_BLOCK, int(wsb.value)), dtype=torch.uint8, device=dev)
                    if self.G > 1 else None)
+
+    def groups(self, cus):
+        """Client groups a launch of this trainer runs on ``cus`` CUs (fs_local_train_plan's rule)."""
+        if self.G <= 1:
+            return 1 if self.chained else self.N
+        if self.chained:
+            return 1
+        per = (self.N + 1) // 2 if self.pair else self.N
+        return max(1, min(per, cus // self.width))
 
     @property
     def shuffler(self):

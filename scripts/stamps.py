@@ -18,6 +18,8 @@ from fedamw_amd import data, engine, rng  # noqa: E402
 from scripts.lt_sweep import SHAPES  # noqa: E402
 
 NAMES = ['fwd', 'S1', 'sum+publish', 'poll+sum', 'next(early)', 'S2', 'softmax+S3+next', 'bwd+update']
+PAIR_NAMES = ['wait rows', 'fwd', 'S1', 'publish+img', 'wait polls', 'check', 'sum+S2', 'softmax+S3',
+              'issue', 'bwd+update']
 
 
 def main():
@@ -25,6 +27,7 @@ def main():
     ap.add_argument('--config', type=int, default=2, choices=sorted(SHAPES))
     ap.add_argument('--G', type=int, default=0)
     ap.add_argument('--chained', action='store_true')
+    ap.add_argument('--pair', action='store_true', help='the pair form at width --G (or the planner\'s)')
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
     sh = SHAPES[a.config]
@@ -33,8 +36,11 @@ def main():
     N, D, C, E, B = sh['clients'], sh['D'], sh['C'], 2, 32
     d = data.federated(N, sh['rows'], D, C, 1000, shape=sh['shape'], device=dev)
     feats = engine.Features(d['X_train'], d['y_train'], D, dev)
-    tr = engine.LocalTrainer(feats, C, B, E, split=(a.G or None), chained=chained)
-    grid = 8 * tr.G if chained else tr.ws.numel() // (2 * tr.G * (16 * 32 + 4) * 8) * tr.G
+    split = (a.G | fedamw_amd._lib.G_PAIR if a.pair else a.G) or None
+    tr = engine.LocalTrainer(feats, C, B, E, split=split, chained=chained)
+    names = PAIR_NAMES if tr.pair else NAMES
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    grid = 8 * tr.width if chained else tr.groups(cus) * tr.width
     extra = grid * 16 * 8
     base = tr.ws.numel() - fedamw_amd._lib.ERR_BLOCK          # exchange granules; stamps go right after
     tr.ws = torch.zeros(tr.ws.numel() + extra, dtype=torch.uint8, device=dev)
@@ -48,13 +54,14 @@ def main():
     st = tr.ws[base:base + extra].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
     st = st[st[:, 15] > 0]
     steps = st[:, 15]
-    per = st[:, :len(NAMES)] / steps[:, None]
-    print('config %d G %d (%s): %d workgroups, %.0f steps each' % (a.config, tr.G, 'chained' if chained else
+    per = st[:, :len(names)] / steps[:, None]
+    print('config %d G %s (%s): %d workgroups, %.0f steps each' % (a.config, ('pair %d' % tr.width) if tr.pair else tr.width, 'chained' if chained else
                                                                    'parallel', len(st), steps.mean()))
-    for k, nm in enumerate(NAMES):
+    for k, nm in enumerate(names):
         print('%-16s mean %8.0f  min %8.0f  max %8.0f cycles/step' % (nm, per[:, k].mean(), per[:, k].min(),
                                                                        per[:, k].max()))
-    print('total            mean %8.0f cycles/step' % per.sum(1).mean(), flush=True)
+    print('total            mean %8.0f cycles/%s' % (per.sum(1).mean(), 'half-step' if tr.pair else 'step'),
+          flush=True)
 
 
 if __name__ == '__main__':

@@ -167,8 +167,8 @@ def test_deferred_eval_uses_idle_cus(amd):
         pytest.skip('not a split launch at this shape')
     E = fed.plan.eval_blocks()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    G, N = fed.trainer.G, len(ys)
-    assert E == min(cus - max(1, min(N, cus // G)) * G, (len(d['y_test']) + 15) // 16) and E > 0
+    tr = fed.trainer
+    assert E == min(cus - tr.groups(cus) * tr.width, (len(d['y_test']) + 15) // 16) and E > 0
     fed.eval_hist.fill_(-7.0)
     fed.round()                                    # evaluation of round 0 deferred
     torch.cuda.synchronize()
