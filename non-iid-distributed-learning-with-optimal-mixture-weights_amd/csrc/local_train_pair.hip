@@ -208,9 +208,8 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
     }
     prow0[L] = lok[L] ? r0 : -1;
   };
-  // labels (wave 0: it writes them to LDS) and the row pieces of lane L's load cursor (of
-  // row 0 when it has none): whatever the lane's state, wave 0 issues RT label loads and every
-  // wave 4 RT row-piece loads
+  // labels (wave 0: it writes them to LDS) and the row bases of lane L's load cursor (row 0
+  // when it has none): whatever the lane's state, wave 0 issues RT label loads
   auto row_src = [&](auto Lc, int rt) {
     constexpr int L = decltype(Lc)::value;
     const int64_t row = prow0[L] >= 0 ? prow0[L] + pr[L][rt] : 0;
@@ -221,17 +220,6 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
     if (w == 0)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) pr_ld1(lb[L][rt], P.labels + (prow0[L] >= 0 ? prow0[L] + pr[L][rt] : 0));
-  };
-  auto issue_rows = [&](auto Lc) {
-    constexpr int L = decltype(Lc)::value;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const float* src = row_src(Lc, rt);
-      pr_ld4<0>(xf[L][rt][0], src);
-      pr_ld4<64>(xf[L][rt][1], src);
-      pr_ld4<128>(xf[L][rt][2], src);
-      pr_ld4<192>(xf[L][rt][3], src);
-    }
   };
 
 #pragma unroll
@@ -253,43 +241,49 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
     for (int rt = 0; rt < RT; ++rt) pr_own(pr[L][rt]);
   issue_labels(std::integral_constant<int, 0>{});
   issue_labels(std::integral_constant<int, 1>{});
-  issue_rows(std::integral_constant<int, 0>{});
-  issue_rows(std::integral_constant<int, 1>{});
+  // lane 0's first rows whole; lane 1's but the last quarter, which half-step 0's forward issues
+  // (as every forward issues the last quarter of the other lane's next rows)
+  constexpr int NP = 4 * RT;                     // row pieces per step and wave
+  const float* srcx[2][RT];                      // row bases of each lane's step being loaded
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    srcx[0][rt] = row_src(std::integral_constant<int, 0>{}, rt);
+    srcx[1][rt] = row_src(std::integral_constant<int, 1>{}, rt);
+  }
+  auto piece = [&](auto Lc, int k) {             // row piece k = (rt, q) of lane L's step being loaded
+    constexpr int L = decltype(Lc)::value;
+    pr_ld4<0>(xf[L][k >> 2][k & 3], srcx[L][k >> 2] + 16 * (k & 3));
+  };
+#pragma unroll
+  for (int k = 0; k < NP; ++k) piece(std::integral_constant<int, 0>{}, k);
+#pragma unroll
+  for (int k = 0; k < 3 * NP / 4; ++k) piece(std::integral_constant<int, 1>{}, k);
 #pragma unroll
   for (int L = 0; L < 2; ++L)
     if (lok[L]) lok[L] = sp_advance<true>(lc[L], P, 2 * grp + L, nvg, T);
   fetch_perm(std::integral_constant<int, 0>{});
   fetch_perm(std::integral_constant<int, 1>{});
   pr_wait<0>();
-  unsigned long long pl[G];                      // polls of the lane published last half-step
+  unsigned long long pl[G - 1];                  // polls of the lane published last half-step (partners)
 #pragma unroll
-  for (int h = 0; h < G; ++h) pl[h] = 0ull;
+  for (int h = 0; h < G - 1; ++h) pl[h] = 0ull;
   lds_barrier();
 
   // Per half-step every wave issues, in this order and whatever the lanes' states (a lane
   // with nothing to publish stores to the dummy slot, one with no next step loads row 0):
-  //   [C] 1 publish store; P1: NP/4 row pieces of lane X's next step; [E] ...; P2: NP/4 more;
-  //   [F] G polls, LBW label loads (wave 0 only: LBW = RT, else 0), RT index loads; P3: the
-  //   last NP/2 pieces, one per other MFMA group of lane Y's backward   (NP = 4 RT)
-  // -- the row stream spread over the half-step at about the rate one CU's memory pipe drains
-  // it, instead of a burst that stalls the issuing waves.  Hence the counted waits: the last
-  // piece of lane X's rows (P3 two half-steps ago) has 1 + NP + G + LBW + RT operations behind
-  // it at [B]; lane Y's polls ([F] one half-step ago) have LBW + RT + NP/2 + 1 + NP/4 at [E].
-  // Extra operations (client-end stores, re-polls) only make a wait stricter.
-  constexpr int NP = 4 * RT;
-  constexpr int WAIT_B0 = 1 + NP + G + RT + RT, WAIT_B = 1 + NP + G + RT;
-  constexpr int WAIT_E0 = RT + RT + NP / 2 + 1 + NP / 4, WAIT_E = RT + NP / 2 + 1 + NP / 4;
+  //   P4: the last NP/4 row pieces of lane Y's next step, one per MFMA group of lane X's
+  //   forward;  [C] 1 publish store;  P1: NP/4 row pieces of lane X's next step;  [E] ...;
+  //   P2: NP/4 more;  [F] G - 1 polls (the partners), LBW label loads (wave 0 only: LBW = RT, else 0), RT index
+  //   loads;  P3: NP/4 more inside lane Y's backward     (NP = 4 RT pieces per step)
+  // -- each lane's next rows spread over two half-steps at about the rate one CU's memory pipe
+  // drains them, never a burst that stalls the issuing waves (and skews the next barrier).
+  // Hence the counted waits: the last piece of lane X's rows (P4 one half-step ago) has
+  // 1 + 3 NP/4 + (G - 1) + LBW + RT operations behind it at [B]; lane Y's polls ([F] one half-step
+  // ago) have LBW + RT + 3 NP/4 + 1 at [E].  Extra operations (client-end stores, re-polls)
+  // only make a wait stricter.
+  constexpr int WAIT_B0 = 1 + 3 * NP / 4 + (G - 1) + RT + RT, WAIT_B = 1 + 3 * NP / 4 + (G - 1) + RT;
+  constexpr int WAIT_E0 = RT + RT + 3 * NP / 4 + 1, WAIT_E = RT + 3 * NP / 4 + 1;
   static_assert(WAIT_B0 < 64, "vmcnt is 6 bits");
-  const float* srcx[2][RT];                      // row bases of each lane's next step (from pr)
-#pragma unroll
-  for (int L = 0; L < 2; ++L)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-      srcx[L][rt] = L == 0 ? row_src(std::integral_constant<int, 0>{}, rt) : row_src(std::integral_constant<int, 1>{}, rt);
-  auto piece = [&](auto Lc, int k) {             // row piece k = (rt, q) of lane L's next step
-    constexpr int L = decltype(Lc)::value;
-    pr_ld4<0>(xf[L][k >> 2][k & 3], srcx[L][k >> 2] + 16 * (k & 3));
-  };
 
 #ifdef FS_STAMPS
   unsigned long long stamp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
@@ -312,16 +306,20 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
 #pragma unroll
       for (int q = 0; q < 4; ++q) pr_own(xf[XL][rt][q]);
     }
-    if (cok[XL]) {
+    {
+      // (the MFMAs run whether or not X has a step: P4's loads sit in one code path; a lane
+      // with nothing to publish publishes zeros)
       floatx4 acc[RT];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4)
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(xf[XL][rt][q][e4], comp(wr[XL][q], e4), acc[rt]);
+        if (RT == 1 ? q == 3 : (q & 1) != 0) piece(Yc, 3 * NP / 4 + (RT == 1 ? 0 : q >> 1));   // P4
+      }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -379,14 +377,14 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
     else pr_wait<WAIT_E>();
     PR_STAMP(5)
 #pragma unroll
-    for (int h = 0; h < G; ++h) pr_own(pl[h]);
+    for (int h = 0; h < G - 1; ++h) pr_own(pl[h]);
     const unsigned tagY = X.tag_base + gsl[YL] + 1u;
     unsigned long long* slotY = xb + (int64_t)((2 * YL + (gsl[YL] & 1)) * G) * X.SZ;
     if (pend[YL]) {
       if (X.spin_limit == 0 && gsl[YL] == 0) dead = true;    // test knob: an injected timeout
       bool ok = true;
 #pragma unroll
-      for (int h = 0; h < G; ++h) ok &= (h == g) | ((unsigned)(pl[h] >> 32) == tagY);
+      for (int h = 0; h < G - 1; ++h) ok &= (unsigned)(pl[h] >> 32) == tagY;
       if (!__all(ok)) {
         unsigned spins = 0;
         for (;;) {
@@ -397,9 +395,9 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
           __builtin_amdgcn_s_sleep(1);
           ok = true;
 #pragma unroll
-          for (int h = 0; h < G; ++h) {
-            pl[h] = pr_poll_now(slotY + (int64_t)h * X.SZ + tid);
-            ok &= (h == g) | ((unsigned)(pl[h] >> 32) == tagY);
+          for (int h = 0; h < G - 1; ++h) {
+            pl[h] = pr_poll_now(slotY + (int64_t)(h < g ? h : h + 1) * X.SZ + tid);
+            ok &= (unsigned)(pl[h] >> 32) == tagY;
           }
           if (__all(ok)) break;
         }
@@ -409,7 +407,12 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
       if (tid < NV) {
         float s = 0.f;
 #pragma unroll
-        for (int h = 0; h < G; ++h) s += (h == g) ? ownv[YL] : __uint_as_float((unsigned)pl[h]);
+        for (int h = 0; h < G; ++h) {              // slice order, the own partial at position g
+          // (partner slice h sits at pl[h] below g and at pl[h - 1] above it: static indices)
+          const float lo = h < G - 1 ? __uint_as_float((unsigned)pl[h < G - 1 ? h : 0]) : 0.f;
+          const float hi = h > 0 ? __uint_as_float((unsigned)pl[h > 0 ? h - 1 : 0]) : 0.f;
+          s += (h == g) ? ownv[YL] : (h < g ? lo : hi);
+        }
         if (tid < NV - 2) {
           const int r = tid / C, c = tid - r * C;
           zsum[r][c] = s;
@@ -436,15 +439,17 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
         float m = valid ? z : -INFINITY;
 #pragma unroll
         for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
-        float se = valid ? expf(z - m) : 0.f;
+        // softmax on v_exp_f32 / v_rcp_f32 / v_log_f32 (one exponential per entry, e / sum e
+        // for the gradient): within the fp32 tolerance of torch's log_softmax (tests/fixtures.py)
+        const float ex = valid ? __expf(z - m) : 0.f;
+        float se = ex;
 #pragma unroll
         for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
         float gv = 0.f;
         if (valid) {
-          const float lp = z - m - logf(se);
           const bool isy = c == lab[YL][r];
-          gv = (isy ? -invb : 0.f) + expf(lp) * invb;
-          if (isy) cep -= lp;
+          gv = (isy ? -invb : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb;
+          if (isy) cep -= z - m - __logf(se);
         }
         gbuf[r][c] = gv;
       }
@@ -460,14 +465,14 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
       unsigned long long* slotP =
           cok[XL] ? xb + (int64_t)((2 * XL + (gsl[XL] & 1)) * G) * X.SZ : dummy;
 #pragma unroll
-      for (int h = 0; h < G; ++h) pr_poll(pl[h], slotP + (int64_t)h * X.SZ + tid);
+      for (int h = 0; h < G - 1; ++h) pr_poll(pl[h], slotP + (int64_t)(h < g ? h : h + 1) * X.SZ + tid);
     }
     issue_labels(Xc);
     if (lok[XL]) lok[XL] = sp_advance<true>(lc[XL], P, 2 * grp + XL, nvg, T);
     fetch_perm(Xc);
     PR_STAMP(9)
 
-    // ---- [G] lane Y: loss, backward (+ P3 of lane X's rows), update.  The backward's MFMAs
+    // ---- [G] lane Y: loss, backward (+ P3 of lane X's next rows), update.  The backward's MFMAs
     // run whether or not Y has a step pending (their result is then dropped), so the row
     // loads sit in ONE code path: their destinations never meet a control-flow merge while
     // in flight (scripts/asm_audit.py) ----
@@ -496,7 +501,7 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
       const float4 x = ld4(img + img_off(4 * kk + lg, RS, w, rblk));
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
-      if (kk & 1) piece(Xc, NP / 2 + (kk >> 1));           // P3
+      if ((kk & 3) == 3) piece(Xc, NP / 2 + (kk >> 2));    // P3
     }
     if (pend[YL]) {
       const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;

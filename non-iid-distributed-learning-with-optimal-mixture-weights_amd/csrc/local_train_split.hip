@@ -415,15 +415,17 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         float m = valid ? z : -INFINITY;
 #pragma unroll
         for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
-        float se = valid ? expf(z - m) : 0.f;
+        // softmax on v_exp_f32 / v_rcp_f32 / v_log_f32 (one exponential per entry, e / sum e
+        // for the gradient): within the fp32 tolerance of torch's log_softmax (tests/fixtures.py)
+        const float ex = valid ? __expf(z - m) : 0.f;
+        float se = ex;
 #pragma unroll
         for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
         float gv = 0.f;
         if (valid) {
-          const float lp = z - m - logf(se);
           const bool isy = c == lab[par][r];
-          gv = (isy ? -invb : 0.f) + expf(lp) * invb;
-          if (isy) cep -= lp;
+          gv = (isy ? -invb : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb;
+          if (isy) cep -= z - m - __logf(se);
         }
         gbuf[r][c] = gv;
       }
