@@ -183,7 +183,8 @@ def stream_ptr(stream=None):
 
 # the device sources each measured kernel is compiled from (its own file + the headers it includes)
 KERNEL_SOURCES = {
-    'local_train': ('local_train.hip', 'local_train_split.hip', 'common.h', 'eval_rows.h', 'lanes.h'),
+    'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_pair.hip', 'split_common.h', 'common.h',
+                    'eval_rows.h', 'lanes.h'),
     'mix_solve': ('mixture.hip', 'common.h', 'lanes.h'),
 }
 

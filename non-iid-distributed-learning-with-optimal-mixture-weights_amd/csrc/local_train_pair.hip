@@ -97,14 +97,11 @@ __device__ __forceinline__ void pr_own(T& x) {
 template <int RT, int G, bool PROX>
 __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParams P, SplitWS X) {
   constexpr int NW = PR_WAVES;
-  constexpr int NTH = PR_THREADS;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
-  constexpr int NZ = NR * NC;
   constexpr int RS = PR_TILES * 64 + 8;          // LDS row stride (floats)
   __shared__ float zpart[NW][NR][NC];
   __shared__ float gbuf[NR][NC];
-  __shared__ float zsum[NR][NC];
   __shared__ int lab[2][NR];
   __shared__ float wred[2][NW][2];
   __shared__ float wce[NW];
@@ -115,7 +112,6 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t ld = P.ld;
   const int C = P.C, B = P.B, E = P.E;
-  const int NV = NR * C + 2;
 
   // fused evaluation blocks (the last fuse_E of the grid): round t-1's test evaluation of
   // W_start on the CUs the groups leave idle (as in the split kernel)
@@ -332,18 +328,19 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
     lds_barrier();  // S1: wave partials; lane X's norms of its previous update
     PR_STAMP(3)
 
-    // ---- [C] publish lane X's partials (thread t owns value t: the B x C logits row-major,
-    // then ||W - W_a||^2 and ||W||^2); every thread stores one granule ----
+    // ---- [C] publish lane X's partials: thread t owns (row, class) = (t / 16, t % 16) -- the
+    // logits at class < C, ||W - W_a||^2 and ||W||^2 at row 0, classes 14 and 15 (C <= 14);
+    // every thread stores one granule ----
     {
       float v = 0.f;
       if (cok[XL]) {
-        if (tid < NV - 2) {
-          const int r = tid / C, c = tid - r * C;
+        const int r = tid >> 4, c = tid & 15;
+        if (r < NR && c < C) {
 #pragma unroll
           for (int i = 0; i < NW; ++i) v += zpart[i][r][c];
-        } else if (tid < NV) {
+        } else if (r == 0 && c >= NC - 2) {
 #pragma unroll
-          for (int i = 0; i < NW; ++i) v += wred[XL][i][tid - (NV - 2)];
+          for (int i = 0; i < NW; ++i) v += wred[XL][i][c - (NC - 2)];
         }
       }
       ownv[XL] = v;
@@ -403,59 +400,49 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
         }
       }
       PR_STAMP(6)
-      // ---- [G] complete lane Y's step: sum the slices in order ----
-      if (tid < NV) {
-        float s = 0.f;
-#pragma unroll
-        for (int h = 0; h < G; ++h) {              // slice order, the own partial at position g
-          // (partner slice h sits at pl[h] below g and at pl[h - 1] above it: static indices)
-          const float lo = h < G - 1 ? __uint_as_float((unsigned)pl[h < G - 1 ? h : 0]) : 0.f;
-          const float hi = h > 0 ? __uint_as_float((unsigned)pl[h > 0 ? h - 1 : 0]) : 0.f;
-          s += (h == g) ? ownv[YL] : (h < g ? lo : hi);
-        }
-        if (tid < NV - 2) {
-          const int r = tid / C, c = tid - r * C;
-          zsum[r][c] = s;
-        } else {
-          nrm[tid - (NV - 2)] = s;                // ||W - W_a||^2, ||W||^2 at the start of the step
-        }
-      }
     }
-    lds_barrier();  // S2: summed logits and norms
 #pragma unroll
     for (int k = NP / 4; k < NP / 2; ++k) piece(Xc, k);    // P2
-    PR_STAMP(7)
+    // ---- [G] complete lane Y's step: sum the slices in order, then -- every value sits at
+    // (row, class) = (tid / 16, tid % 16), a row on one 16-lane DPP row -- the softmax straight
+    // from the registers (no LDS round trip, no barrier) ----
     // (a lane with nothing pending may have an exhausted cursor: its fields are not used)
     const int st = pend[YL] ? cc[YL].st : 0, nbat = pend[YL] ? cc[YL].nbat : 1, n = pend[YL] ? cc[YL].n : 1;
     const int e = st / nbat, sb = st - e * nbat;
     const int bc = max(1, min(B, n - sb * B));
     const float invb = 1.0f / (float)bc;
     if (pend[YL]) {
-      float cep = 0.f;
-      for (int idx = tid; idx < NZ; idx += NTH) {          // NC lanes of one wave hold one row
-        const int r = idx / NC, c = idx - r * NC;
-        const bool valid = r < bc && c < C;
-        const float z = valid ? zsum[r][c] : 0.f;
-        float m = valid ? z : -INFINITY;
+      float z = 0.f;
 #pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
-        // softmax on v_exp_f32 / v_rcp_f32 / v_log_f32 (one exponential per entry, e / sum e
-        // for the gradient): within the fp32 tolerance of torch's log_softmax (tests/fixtures.py)
-        const float ex = valid ? __expf(z - m) : 0.f;
-        float se = ex;
-#pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
-        float gv = 0.f;
-        if (valid) {
-          const bool isy = c == lab[YL][r];
-          gv = (isy ? -invb : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb;
-          if (isy) cep -= z - m - __logf(se);
-        }
-        gbuf[r][c] = gv;
+      for (int h = 0; h < G; ++h) {                // slice order, the own partial at position g
+        // (partner slice h sits at pl[h] below g and at pl[h - 1] above it: static indices)
+        const float lo = h < G - 1 ? __uint_as_float((unsigned)pl[h < G - 1 ? h : 0]) : 0.f;
+        const float hi = h > 0 ? __uint_as_float((unsigned)pl[h > 0 ? h - 1 : 0]) : 0.f;
+        z += (h == g) ? ownv[YL] : (h < g ? lo : hi);
       }
+      const int r = tid >> 4, c = tid & 15;
+      if (r == 0 && c >= NC - 2) nrm[c - (NC - 2)] = z;   // ||W - W_a||^2, ||W||^2 at the step's start
+      const bool valid = r < bc && c < C;
+      float m = valid ? z : -INFINITY;
+#pragma unroll
+      for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
+      // softmax on v_exp_f32 / v_rcp_f32 / v_log_f32 (one exponential per entry, e / sum e for
+      // the gradient): within the fp32 tolerance of torch's log_softmax (tests/fixtures.py)
+      const float ex = valid ? __expf(z - m) : 0.f;
+      float se = ex;
+#pragma unroll
+      for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
+      float gv = 0.f, cep = 0.f;
+      if (valid) {
+        const bool isy = c == lab[YL][r];
+        gv = (isy ? -invb : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb;
+        if (isy) cep = -(z - m - __logf(se));
+      }
+      if (r < NR) gbuf[r][c] = gv;
       cep = wave_sum_dpp(cep, lane);
       if (lane == 0) wce[w] = cep;
     }
+    PR_STAMP(7)
     lds_barrier();  // S3: g, CE partials
     PR_STAMP(8)
 
@@ -573,16 +560,16 @@ static size_t pair_dyn_lds(int RT) { return sizeof(float) * 2 * (size_t)(RT * 16
 
 static size_t pair_static_lds(int RT) {
   const int NR = RT * 16;
-  return (size_t)PR_WAVES * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + 2 * PR_WAVES * 2 * 4 +
+  return (size_t)PR_WAVES * NR * 16 * 4 + (size_t)NR * 16 * 4 + 2 * NR * 4 + 2 * PR_WAVES * 2 * 4 +
          PR_WAVES * 4 + 8 + 64;
 }
 
 // can the pair kernel run this shape with groups of G workgroups?
 bool pair_fits(int C, int B, int NT, int G) {
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
-  if (C > 16 || B > 32 || NT != PR_TILES * G) return false;
+  // C <= 14: the two norms travel at classes 14 and 15 of row 0 of the (row, class) hand-off
+  if (C > 14 || B > 32 || NT != PR_TILES * G) return false;
   const int RT = pair_rt(B);
-  if (RT * 16 * C + 2 > PR_THREADS) return false;   // one exchanged value per thread
   return pair_dyn_lds(RT) + pair_static_lds(RT) <= 160 * 1024;
 }
 
@@ -613,7 +600,7 @@ int launch_local_train_pair(const LTParams& P, int G, void* ws, int64_t ws_bytes
   const int NT = (int)(P.ld >> 6);
   if (P.chained) return fail(FS_EINVAL, "fs_local_train: the pair form needs parallel clients");
   if (!pair_fits(P.C, P.B, NT, G))
-    return fail(FS_EUNSUPPORTED, "fs_local_train: the pair form needs C <= 16, B <= 32 and ld == 512 G");
+    return fail(FS_EUNSUPPORTED, "fs_local_train: the pair form needs C <= 14, B <= 32 and ld == 512 G");
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
   if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");
