@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
   "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "$REGEX" -d $OUT/p$i -o p$i --output-format csv \
+  timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-include-regex "$REGEX" -d $OUT/p$i -o p$i --output-format csv \
     -- python3 -u bench.py $ARGS --no-cpu-baseline > $OUT/p$i.log 2>&1
   rc=$?
   echo "pmc $TAG pass $i ($grp) rc=$rc"
