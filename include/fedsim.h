@@ -217,16 +217,17 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * torch.optim.SGD starts empty, tools.py:423).  A single persistent workgroup
  * where a register-resident instance covers (N, C, Bv) -- for N <= 128 the quarter-wave
  * solver (4 batch rows per wave), with 4 L2 prefetch helper workgroups on its XCD that
- * only load (FS_MIX_PF_H=<n> sets their number, 0 = none; their progress word is byte
- * 128 of the error block); otherwise (Bv <= 16,
- * C <= 16, N <= 2048) K <= 32 workgroups that split the clients and exchange
- * partial logits every step (slices of S >= 16 clients: reduce-scatter to owner workgroups, then an
- * all-gather of the totals; FS_MIX_MC_HOPS=1 forces the one-hop all-to-all);
- * otherwise one LDS-staged / global workgroup.
+ * only load (fs_tuning.mix_prefetch sets their number, -1 = none; their progress word is
+ * byte 128 of the error block); for N > 256 the multi-CU quarter-wave solver "qmc"
+ * (K <= 16 workgroups of 128 clients on one XCD, one exchange hop per step, 16 helper
+ * workgroups); otherwise (Bv <= 16, C <= 16, N <= 2048) K <= 32 workgroups that split the
+ * clients and exchange partial logits every step (slices of S >= 16 clients: reduce-scatter
+ * to owner workgroups, then an all-gather of the totals); otherwise one LDS-staged /
+ * global workgroup.
  * d_ws: fs_mix_solve_ws_bytes(N, C, Bv) bytes, zeroed once at allocation (the multi-CU
  * exchange granules + the error block; a timed-out exchange also writes NaN into d_p).
- * Concurrent solves need separate workspaces.  FS_MIX_SOLVER=wave|quad|reg2|reg|mc|staged|global
- * forces one solver (FS_MIX_SWAP=0: reg2 without the permlane swap-add levels).
+ * Concurrent solves need separate workspaces.  fs_tuning.mix_solver (FS_SOLVER_*) forces a
+ * solver (tests, diagnostics; one that does not cover the shape falls through).
  * ------------------------------------------------------------------------- */
 int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv);
 int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
@@ -234,10 +235,10 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
                  int* d_first, void* d_ws, int64_t ws_bytes, void* stream);
 
 /* Diagnostic (host state only): the solver the calling thread's last fs_mix_solve
- * launched -- 1 register-resident (one row per wave), 2 multi-CU, 3 LDS-staged, 4 global,
- * 5 register-resident form 2 (two rows per wave, Bv <= 16, C <= 10), 6 one wave (N <= 16,
- * C <= 4, Bv <= 16), 7 row-split (forced only), 8 quarter-wave (N <= 64 with C <= 16, or
- * N <= 128 with C <= 10; Bv <= 16); 0 = none yet. */
+ * launched -- FS_SOLVER_REG (1, register-resident, one row per wave), _MC (2, multi-CU),
+ * _STAGED (3), _GLOBAL (4), _REG2 (5, two rows per wave, Bv <= 16, C <= 10), _WAVE (6, one
+ * wave: N <= 16, C <= 4, Bv <= 16), _QUAD (8, quarter-wave: N <= 64 with C <= 16, or N <= 128
+ * with C <= 10; Bv <= 16), _QMC (9, multi-CU quarter-wave); 0 = none yet. */
 int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *
@@ -362,7 +363,8 @@ int fs_plan_set_shuffle_chunk(fs_plan* plan, int rounds);
 /* ABI 7: launch a partly collected chunk now (after preparing a run's last round). */
 int fs_plan_shuffle_flush(fs_plan* plan);
 /* ABI 8: evaluation workgroups a TRAIN launch of this plan carries for FS_PHASE_EVAL_DEFER
- * (0: the plan evaluates with launches of its own; FS_EVAL_FUSE=0 at creation forces 0). */
+ * (0: the plan evaluates with launches of its own; fs_tuning.no_eval_fuse = 1 at creation
+ * forces 0). */
 int fs_plan_eval_blocks(const fs_plan* plan);
 
 /* ABI 7, measurement: timing events recorded without a system-scope release (so timing a
