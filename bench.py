@@ -197,8 +197,8 @@ def setup_rank(args):
         if float(t.item()) != want:
             raise SystemExit('bench: all-reduce sanity check gave %r, expected %r' % (float(t.item()), want))
         ids = [None] * ws
-        tdist.all_gather_object(ids, (socket.gethostname(), torch.cuda.get_device_properties(dev).uuid
-                                      if hasattr(torch.cuda.get_device_properties(dev), 'uuid') else local))
+        props = torch.cuda.get_device_properties(dev)
+        tdist.all_gather_object(ids, (socket.gethostname(), str(props.uuid) if hasattr(props, 'uuid') else local))
         info = {'backend': tdist.get_backend(), 'world_size': tdist.get_world_size(),
                 'devices': len(set(str(i) for i in ids)), 'allreduce_check': float(t.item()),
                 'rehearsal': backend == 'gloo'}
@@ -472,6 +472,11 @@ def _solver_name():
 
 
 def worker(args):
+    # the JSON line is this process's only stdout: anything else -- gloo's / RCCL's connection
+    # messages, library warnings -- goes to stderr (fd 1 is pointed at fd 2 for the whole run)
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
     import torch
     import torch.distributed as tdist
     import fedamw_amd  # noqa: F401
@@ -524,7 +529,7 @@ def worker(args):
                 print('bench: config %d leg %.1f s, %.0f client-rounds/s' % (cfg, obj['leg_wall_s'], obj['value']),
                       file=sys.stderr, flush=True)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=line_out, flush=True)
     if ws > 1:
         tdist.barrier()
         tdist.destroy_process_group()

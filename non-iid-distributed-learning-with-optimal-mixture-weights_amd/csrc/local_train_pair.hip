@@ -100,7 +100,10 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int RS = PR_TILES * 64 + 8;          // LDS row stride (floats)
-  __shared__ float zpart[NW][NR][NC];
+  // wave partial logits in the MFMA accumulator's own layout, [rt][lg][class][i] = row
+  // 16 rt + 4 lg + i: one conflict-free ds_write_b128 per row tile, and the (row, class)
+  // reads of the publish stride 4 words across a 16-lane row (conflict-free too)
+  __shared__ __attribute__((aligned(16))) float zpart[NW][NR * NC];
   __shared__ float gbuf[NR][NC];
   __shared__ int lab[2][NR];
   __shared__ float wred[2][NW][2];
@@ -318,8 +321,7 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
       }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
+        st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
     }
     // lane X's next step: row bases from its indices (fetched two half-steps ago)
 #pragma unroll
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
         const int r = tid >> 4, c = tid & 15;
         if (r < NR && c < C) {
 #pragma unroll
-          for (int i = 0; i < NW; ++i) v += zpart[i][r][c];
+          for (int i = 0; i < NW; ++i) v += zpart[i][zp_off(r, c)];
         } else if (r == 0 && c >= NC - 2) {
 #pragma unroll
           for (int i = 0; i < NW; ++i) v += wred[XL][i][c - (NC - 2)];

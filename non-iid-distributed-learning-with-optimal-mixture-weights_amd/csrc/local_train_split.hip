@@ -89,7 +89,10 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
   constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
   constexpr int HC = G;                             // partners polled per round trip
-  __shared__ float zpart[NW][NR][NC];
+  // wave partial logits in the MFMA accumulator's own layout, [rt][lg][class][i] = row
+  // 16 rt + 4 lg + i: one conflict-free ds_write_b128 per row tile, and the (row, class)
+  // reads of the publish stride 4 words across a 16-lane row (conflict-free too)
+  __shared__ __attribute__((aligned(16))) float zpart[NW][NR * NC];
   __shared__ float gbuf[NR][NC];
   __shared__ float zsum[NR][NC];
   __shared__ int lab[2][NR];
@@ -309,8 +312,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) zpart[w][rt * 16 + 4 * lg + i][l16] = acc[rt][i];
+        st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
       SP_STAMP(1)
       lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           if (idx < NV - 2) {
             const int r = idx / C, c = idx - r * C;
 #pragma unroll
-            for (int i = 0; i < NW; ++i) v += zpart[i][r][c];
+            for (int i = 0; i < NW; ++i) v += zpart[i][zp_off(r, c)];
           } else if (idx < NV) {
 #pragma unroll
             for (int i = 0; i < NW; ++i) v += wred[i][idx - (NV - 2)];

@@ -57,6 +57,9 @@ __device__ __forceinline__ int64_t tab_i64(const int64_t* base, int i) {
   return v;
 }
 
+// offset of (row, class) in a wave's partial-logit block [rt][lg][class][i] (row = 16 rt + 4 lg + i)
+__device__ __forceinline__ int zp_off(int r, int c) { return (r >> 4) * 256 + ((r >> 2) & 3) * 64 + c * 4 + (r & 3); }
+
 // Client k of a group's sequence (-1: none).  Parallel: tier k of the LPT-ordered clients,
 // snake order (even tiers forward, odd tiers backward) so the groups' step totals balance.
 template <bool SC = false>
