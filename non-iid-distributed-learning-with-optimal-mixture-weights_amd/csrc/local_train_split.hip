@@ -476,9 +476,17 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           floatx4 ga[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) ga[e4] = floatx4{0.f, 0.f, 0.f, 0.f};
+          // image row 4 kk + lg, block rblk ^ (4 (kk & 1) + lg): two per-lane bases (kk even / odd)
+          // and, in the FULL instance (compile-time row stride), the rows as immediate offsets --
+          // 16 hoisted addresses per tile spilled at G = 16 and each reload waited vmcnt(0) for
+          // the whole row stream inside this loop
+          constexpr int RS_FULL = NW * TPW * 64 + 8;
+          const int RSx = decltype(FULL)::value ? RS_FULL : RS;
+          const float* ib0 = xs_lds + lg * RSx + 64 * Tl + 4 * (rblk ^ lg);
+          const float* ib1 = xs_lds + lg * RSx + 64 * Tl + 4 * (rblk ^ (lg + 4));
 #pragma unroll
           for (int kk = 0; kk < 4 * RT; ++kk) {
-            const float4 x = ld4(xs_lds + img_off(4 * kk + lg, RS, Tl, rblk));
+            const float4 x = ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RSx);
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
             if constexpr (decltype(LD)::value)
