@@ -79,6 +79,7 @@ const char* fs_last_error(void);
 #define FS_SOLVER_WAVE 6
 #define FS_SOLVER_QUAD 8
 #define FS_SOLVER_QMC 9
+#define FS_SOLVER_BIN 10
 
 typedef struct fs_tuning {
   int mix_solver;
@@ -215,7 +216,8 @@ int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int 
  * buf = first ? grad : momentum*buf + grad; p -= lr_p*buf.  d_p, d_buf [N] are
  * updated in place; *d_first (int) is read and cleared (the momentum buffer of
  * torch.optim.SGD starts empty, tools.py:423).  A single persistent workgroup
- * where a register-resident instance covers (N, C, Bv) -- for N <= 128 the quarter-wave
+ * where a register-resident instance covers (N, C, Bv) -- for N <= 16 with C <= 2 one wave
+ * ("bin", no LDS, no barrier); for N <= 128 the quarter-wave
  * solver (4 batch rows per wave), with 4 L2 prefetch helper workgroups on its XCD that
  * only load (fs_tuning.mix_prefetch sets their number, -1 = none; their progress word is
  * byte 128 of the error block); for N > 256 the multi-CU quarter-wave solver "qmc"
@@ -238,7 +240,8 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
  * launched -- FS_SOLVER_REG (1, register-resident, one row per wave), _MC (2, multi-CU),
  * _STAGED (3), _GLOBAL (4), _REG2 (5, two rows per wave, Bv <= 16, C <= 10), _WAVE (6, one
  * wave: N <= 16, C <= 4, Bv <= 16), _QUAD (8, quarter-wave: N <= 64 with C <= 16, or N <= 128
- * with C <= 10; Bv <= 16), _QMC (9, multi-CU quarter-wave); 0 = none yet. */
+ * with C <= 10; Bv <= 16), _QMC (9, multi-CU quarter-wave), _BIN (10, one wave, two classes:
+ * N <= 16, C <= 2, Bv <= 16); 0 = none yet. */
 int fs_mix_solve_last_mode(void);
 
 /* ------------------------------------------------------------------------- *

@@ -67,7 +67,7 @@ ABI_VERSION = 10
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
-SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc'}
+SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc', 10: 'bin'}
 SOLVERS = {v: k for k, v in SOLVER_NAMES.items() if k}
 
 

@@ -1267,6 +1267,170 @@ __global__ __launch_bounds__(64) void mix_solve_wave_kernel(const float* __restr
 }
 
 // ----------------------------------------------------------------------------
+// p-solve, one wave for two classes ("bin": N <= 16, C <= 2, Bv <= 16 -- config 1's FedAMW on
+// a9a, N = 10, C = 2).  `wave` above gives half its lanes to padding classes and runs its
+// softmax on libm; `quad` pays an LDS barrier per step for 4 waves.  Here lane l = (row b = l/4,
+// class c = (l/2) & 1, half h = l & 1) holds 8 of the 16 client columns (8h .. 8h+7) of its
+// (row, class) segment -- 2 float4 -- and p of those 8 clients in VGPRs:
+//   * logit: a packed 8-term dot product plus one DPP add over the half pair (o_0 + o_1 in
+//     both lanes: the same bits);
+//   * softmax of two classes: the other class's logit by one DPP move, g = rcp(1 + exp(o' - o))
+//     on v_exp_f32 / v_rcp_f32 (fs_tuning.mix_exact_softmax = 1: torch's exp(o - m - log(e0 +
+//     e1)) on libm), minus the label's one-hot, over the batch size;
+//   * gradient: 8 packed products reduce-scattered over row bits 5, 4 (permlane32 / 16 swaps)
+//     and 3 (bank-masked DPP adds), then summed over row bit 2 and the class bit, so that lane
+//     l ends with client 8h + 4 bit5 + 2 bit4 + bit3's total (4 lanes each, the same bits);
+//   * the momentum step there, and the inverse moves (DPP, then the swaps) gather p back to
+//     8 clients per lane.
+// No LDS, no barrier, no SGPR round trip.  Z through a buffer descriptor (a chunk past ldN or
+// a padding class reads zeros), a DEPTH-step register ring; row indices DEPTH steps earlier.
+// ----------------------------------------------------------------------------
+constexpr int MB_DEPTH = 8;
+
+template <bool FASTX>
+__global__ __launch_bounds__(64) void mix_solve_bin_kernel(const float* __restrict__ Z, const int32_t* __restrict__ y,
+                                                           const int32_t* __restrict__ perms, int N, int C, int nv,
+                                                           int epochs, int Bv, float lr, float mom,
+                                                           float* __restrict__ p, float* __restrict__ buf,
+                                                           int* __restrict__ first_flag, int z_bytes) {
+  static_assert(MB_DEPTH * 4 <= 63, "ring vs the vmcnt window");
+  const int lane = threadIdx.x;
+  const int b = lane >> 2, c = (lane >> 1) & 1, h = lane & 1;
+  const int ldN = mix_ldn(N);                      // <= 16
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int bc_tail = nv - (nbat - 1) * Bv;
+  const float invB = 1.0f / (float)Bv;
+  const float invT = 1.0f / (float)bc_tail;
+  const bool real = c < C;
+  uint32_t lofs[2];                                // byte offsets of the lane's chunks in a row
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int col = 8 * h + 4 * k;
+    lofs[k] = (real && col < ldN) ? 4u * (uint32_t)(c * ldN + col) : 0x80000000u;
+  }
+  // the client this lane holds after the reduce-scatter; p of the lane's 8 dot-product clients
+  const int kn = 8 * h + 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+  float po = kn < N ? p[kn] : 0.f;
+  float bo = kn < N ? buf[kn] : 0.f;
+  float pv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pv[j] = 8 * h + j < N ? p[8 * h + j] : 0.f;   // p = 0 on padding
+  int first = *first_flag;
+  const bool b3 = (lane >> 3) & 1;
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
+  // fetch cursor: the step whose row indices are read next (stays on the last step at the end)
+  int fst = 0, fep = 0, fsb = 0;
+  auto fetch_row = [&]() -> int {
+    const int base = fep * nv + fsb * Bv;
+    const int bc = min(Bv, nv - fsb * Bv);
+    const int row = perms[base + (b < bc ? b : 0)];   // rows past the batch: its first (masked)
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+    return row;
+  };
+  floatx4 zr[MB_DEPTH][2];
+  int idxq[MB_DEPTH], labq[MB_DEPTH];
+#define MB_ISSUE(R_, ROW_)                                                                   \
+  {                                                                                          \
+    const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
+    _Pragma("unroll") for (int k = 0; k < 2; ++k) zr[R_][k] =                                \
+        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[k], 0, 0)); \
+  }
+#pragma unroll
+  for (int k = 0; k < MB_DEPTH; ++k) {
+    const int row = fetch_row();
+    labq[k] = y[row];
+    MB_ISSUE(k, row);
+  }
+#pragma unroll
+  for (int k = 0; k < MB_DEPTH; ++k) idxq[k] = fetch_row();
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): the loop inherits only its own order
+  int csb = 0;
+  int s = 0;
+#define MB_STEP(R_, TAIL_)                                                                   \
+  {                                                                                          \
+    if (TAIL_ && s >= total) break;                                                          \
+    const int bc = min(Bv, nv - csb * Bv);                                                   \
+    const float invb = bc == Bv ? invB : invT;                                               \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
+    float2v a2 = {0.f, 0.f};                                                                 \
+    _Pragma("unroll") for (int j = 0; j < 8; j += 2) a2 = __builtin_elementwise_fma(          \
+        half2(zr[R_][j >> 2], (j >> 1) & 1), float2v{pv[j], pv[j + 1]}, a2);                 \
+    const float op = a2.x + a2.y;                                                            \
+    const float o = op + dpp<0xB1>(op);              /* the half pair: quad_perm [1,0,3,2] */ \
+    const float oo = C > 1 ? dpp<0x4E>(o) : -INFINITY;   /* the other class: [2,3,0,1] */    \
+    float sm;                                                                                \
+    if constexpr (FASTX) {                                                                   \
+      sm = __builtin_amdgcn_rcpf(1.f + __expf(oo - o));                                      \
+    } else {                       /* torch's log_softmax backward: exp(o - m - log(sum)) */ \
+      const float m = fmaxf(o, oo);                                                          \
+      sm = expf(o - m - logf(expf(o - m) + expf(oo - m)));                                   \
+    }                                                                                        \
+    const float g = (real && b < bc) ? (c == labq[R_] ? -invb : 0.f) + sm * invb : 0.f;      \
+    float v[8];                                                                              \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                          \
+      float2v t2 = float2v{g, g} * half2(zr[R_][j >> 1], j & 1);                             \
+      asm volatile("" : "+v"(t2));                   /* computed here: the slot dies here */ \
+      v[2 * j] = t2.x;                                                                       \
+      v[2 * j + 1] = t2.y;                                                                   \
+    }                                                                                        \
+    /* slot consumed: refill with step s + DEPTH, then fetch the rows of s + 2 DEPTH (the   \
+       scheduling fence keeps the refill below the slot's last use: one register per slot,   \
+       no copies on the loop's back edge) */                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    labq[R_] = y[idxq[R_]];                                                                  \
+    MB_ISSUE(R_, idxq[R_]);                                                                  \
+    idxq[R_] = fetch_row();                                                                  \
+    float t[4];                                                                              \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) t[i] = rs_level<32, true>(v[i], v[i + 4], lane); \
+    const float u0 = rs_level<16, true>(t[0], t[2], lane);                                   \
+    const float u1 = rs_level<16, true>(t[1], t[3], lane);                                   \
+    float gs = rs_bank<8>(u0, u1);                                                           \
+    gs = rs_bank<4>(gs, gs);                         /* over row bit 2 */                    \
+    gs = gs + dpp<0x4E>(gs);                         /* over the class bit */                \
+    if (kn < N) momentum_step(po, bo, gs, first, mom, lr);                                   \
+    first = 0;                                                                               \
+    /* gather p back: row bit 3 (row_ror:8), then bits 4 and 5 (swaps) */                   \
+    const float px = dpp<0x128>(po);                                                         \
+    float r4[4];                                                                             \
+    gather_pair<16>(b3 ? px : po, r4[0], r4[2]);                                             \
+    gather_pair<16>(b3 ? po : px, r4[1], r4[3]);                                             \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) gather_pair<32>(r4[i], pv[i], pv[i + 4]); \
+    ++s;                                                                                     \
+  }
+  // whole ring turns without an exit inside (a break per step gives the loop a latch shared
+  // with the exits, where hipcc copies the ring registers and waits for the newest loads),
+  // then the last total % DEPTH steps
+  for (int it = total / MB_DEPTH; it > 0; --it) {
+    MB_STEP(0, false) MB_STEP(1, false) MB_STEP(2, false) MB_STEP(3, false)
+    MB_STEP(4, false) MB_STEP(5, false) MB_STEP(6, false) MB_STEP(7, false)
+  }
+  do {
+    MB_STEP(0, true) MB_STEP(1, true) MB_STEP(2, true) MB_STEP(3, true)
+    MB_STEP(4, true) MB_STEP(5, true) MB_STEP(6, true)
+  } while (false);
+#undef MB_STEP
+#undef MB_ISSUE
+  if ((lane & 6) == 0 && kn < N) {                 // one of the 4 lanes holding client kn
+    p[kn] = po;
+    buf[kn] = bo;
+  }
+  if (lane == 0 && total > 0) *first_flag = 0;
+}
+
+static bool bin_covers(int N, int C, int Bv, int nv, int epochs) {
+  const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
+  return N <= 16 && C <= 2 && Bv <= 16 && zb < ((int64_t)1 << 31) && (int64_t)epochs * nv < ((int64_t)1 << 31);
+}
+
+// ----------------------------------------------------------------------------
 // p-solve, multi-CU form (Bv <= 16, C <= 16, N <= 2048).  One workgroup on one CU cannot
 // stream a batch of Z rows faster than ~33 GB/s (gathered rows from the Infinity Cache,
 // MI355X_MICROARCH.md "Indexed rows"): at config 2 that is 64 KB per step, ~2 us -- the
@@ -1876,8 +2040,8 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   const fs_tuning tune = tuning();
   const int want = tune.mix_solver;
   const bool aut = want == FS_SOLVER_AUTO;
-  // one wave where it measured fastest (N <= 16, C = 3..4: 0.616 vs 0.62 us per step); the
-  // quarter-wave solver from C <= 2 (config 1, N = 10: 0.574 vs 0.617 us, r02s2c1b) upwards
+  // two classes, N <= 16 (config 1): the one-wave binary solver; one wave where it measured
+  // fastest (N <= 16, C = 3..4: 0.616 vs 0.62 us per step); else the quarter-wave solver
   const bool auto_wave = N <= 16 && C >= 3 && C <= 4 && Bv <= 16;
   const bool use_quad = (aut && !auto_wave && quad_covers(N, C, Bv, n_val, epochs)) || want == FS_SOLVER_QUAD;
   // the multi-CU quarter-wave solver where the single-workgroup register solvers end (N > 256)
@@ -1911,6 +2075,18 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // solver (one exchange hop per step; 3.9 us at N = 1000, C = 10) where it covers, else the
   // multi-CU solver (two hops, ~4-7 us per step, 7-11x the single-workgroup staged / global
   // solvers at N = 200..1000, C = 10); else those.
+  if (((aut && N <= 16 && C <= 2) || want == FS_SOLVER_BIN) && bin_covers(N, C, Bv, n_val, epochs)) {
+    const int zb = (int)((int64_t)n_val * C * mix_ldn(N) * 4);
+    if (!tune.mix_exact_softmax)
+      hipLaunchKernelGGL(mix_solve_bin_kernel<true>, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val,
+                         epochs, Bv, lr_p, momentum, d_p, d_buf, d_first, zb);
+    else
+      hipLaunchKernelGGL(mix_solve_bin_kernel<false>, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val,
+                         epochs, Bv, lr_p, momentum, d_p, d_buf, d_first, zb);
+    t_last_solver = FS_SOLVER_BIN;
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
   if (((aut && auto_wave) || want == FS_SOLVER_WAVE) && N <= 16 && C <= 4 && Bv <= 16) {
     hipLaunchKernelGGL(mix_solve_wave_kernel, dim3(1), dim3(64), 0, st0, d_Z, d_labels, d_perms, N, C, n_val, epochs,
                        Bv, lr_p, momentum, d_p, d_buf, d_first);

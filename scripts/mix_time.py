@@ -1,5 +1,6 @@
 """Diagnostic: fs_mix_solve time per dependent p-SGD step (and fs_mix_z) at a given shape.
-    python scripts/mix_time.py [N] [C] [n_val] [epochs]      (GPU box; default config 2)"""
+    [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] python scripts/mix_time.py [N] [C] [n_val] [epochs]
+(GPU box; default config 2; the two variables only select fs_tuning fields for this run)"""
 import os
 import sys
 
@@ -10,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import fedamw_amd  # noqa: E402,F401
 from fedamw_amd import engine, rng  # noqa: E402
 
+SOLVER = os.environ.get('FS_MIX_SOLVER', 'auto')
+fedamw_amd._lib.set_tuning(mix_solver=SOLVER, mix_exact_softmax=int(os.environ.get('FS_MIX_EXACT', '0')))
 a = [int(x) for x in sys.argv[1:]]
 N, C, nv, ep = (a + [100, 10, 12800, 10][len(a):])[:4]
 D = 2048
@@ -48,12 +51,12 @@ print('N=%d C=%d n_val=%d epochs=%d: mix_z %.1f us (%.1f TFLOP/s), mix_solve %.2
       'p finite: %s' % (N, C, nv, ep, zms * 1e3, 2.0 * N * C * D * nv / zms / 1e9, sms, sms * 1e3 / steps, steps,
                         bool(torch.isfinite(mix.p).all())), flush=True)
 mix.check_errors()
-print('  solver requested %s, ran %s' % (os.environ.get('FS_MIX_SOLVER', 'auto'),
+print('  solver requested %s, ran %s' % (SOLVER,
                                          L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]), flush=True)
 if STAMPS:
     acc = mix.buf[N + 8:N + 20].cpu().numpy().view(np.uint64)
     names = (['wait+logits', 'rs+softmax+grad', 'fold', 'barrier', 'update+gather', 'issue']
-             if os.environ.get('FS_MIX_SOLVER') == 'quad' else
+             if SOLVER == 'quad' else
              ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update'])
     print('wave-0 s_memtime ticks per step (last call): ' +
           ', '.join('%s %.0f' % (nm, a / steps) for nm, a in zip(names, acc)), flush=True)

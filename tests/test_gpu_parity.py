@@ -393,7 +393,7 @@ def test_eval_unit_golden(amd):
 
 
 @pytest.mark.parametrize('N,C,nv,Bv', [
-    (10, 2, 203, 16),       # config 1 shape: quarter-wave solver (C <= 2)
+    (10, 2, 203, 16),       # config 1 shape: the one-wave binary solver (C <= 2)
     (16, 4, 77, 16),        # one wave, every lane's class real, ragged last batch
     (5, 3, 40, 7),          # one wave, Bv < 16 (idle rows), N not a multiple of 4
     (1, 2, 33, 16),         # one client
@@ -435,7 +435,8 @@ def test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.5):
         assert ep <= 1e-5 and eb <= 1e-4, (rnd, ep, eb)
 
 
-@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'quad'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
+@pytest.mark.parametrize('N,C,Bv,solver', [(10, 2, 16, 'bin'), (16, 4, 16, 'wave'), (17, 4, 16, 'quad'),
+                                           (16, 2, 16, 'bin'), (17, 2, 16, 'quad'), (16, 2, 17, 'staged'),
                                            (10, 5, 16, 'quad'), (100, 10, 16, 'quad'), (64, 16, 16, 'quad'),
                                            (37, 20, 16, 'reg'), (129, 3, 16, 'reg2'), (200, 4, 16, 'reg2'),
                                            (1000, 10, 16, 'qmc'), (300, 4, 16, 'qmc'), (1100, 16, 16, 'mc'),
@@ -525,6 +526,23 @@ def test_mix_solve_quad(amd, N, C, nv, Bv):
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
 
 
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (10, 2, 203, 16),       # config 1 shape: 2 of each lane's 4 chunks past ldN = 12 read zeros
+    (16, 2, 77, 16),        # every chunk real, ragged last batch
+    (5, 2, 40, 7),          # Bv = 7: idle rows, N not a multiple of 4 (ldN = 8: half h = 1 all padding)
+    (1, 2, 33, 16),         # one client
+    (13, 2, 1000, 16),      # 63 steps per epoch: ring turns + a 7-step tail
+    (8, 2, 16, 16),         # one batch per epoch (total = 2 steps: tail only)
+])
+@pytest.mark.parametrize('exact', [0, 1])
+def test_mix_solve_bin(amd, N, C, nv, Bv, exact):
+    """fs_mix_solve's one-wave binary solver (lane = row x class x client half; default
+    v_exp / v_rcp softmax and torch's libm form) vs the oracle's p-SGD, 2 rounds x 2 epochs."""
+    with amd.lib.tuning(mix_solver='bin', mix_exact_softmax=exact):
+        test_mix_solve_variants(amd, N, C, nv, Bv)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'bin'
+
+
 @pytest.mark.parametrize('N,C,nv,Bv', [(100, 10, 517, 16), (60, 8, 33, 9), (37, 16, 90, 16)])
 def test_mix_solve_quad_libm_softmax(amd, N, C, nv, Bv):
     """The quarter-wave solver with torch's softmax form on libm expf / logf
@@ -574,7 +592,7 @@ def test_mix_solve_prefetch_helpers(amd, N, C, nv, Bv, h, lead, solver):
 
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
                                         ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('wave', 10, 2),
-                                        ('reg2', 100, 10)])
+                                        ('quad', 10, 2), ('reg2', 100, 10)])
 def test_mix_solve_forced_fallbacks(amd, solver, N, C):
     """The solvers the auto choice does not take at these shapes, forced through fs_tuning."""
     with amd.lib.tuning(mix_solver=solver):
