@@ -1340,8 +1340,8 @@ __global__ __launch_bounds__(64) void mix_solve_bin_kernel(const float* __restri
 #define MB_ISSUE(R_, ROW_)                                                                   \
   {                                                                                          \
     const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
-    _Pragma("unroll") for (int k = 0; k < 2; ++k) zr[R_][k] =                                \
-        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[k], 0, 0)); \
+    _Pragma("unroll") for (int k_ = 0; k_ < 2; ++k_) zr[R_][k_] =                            \
+        __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[k_], 0, 0)); \
   }
 #pragma unroll
   for (int k = 0; k < MB_DEPTH; ++k) {
