@@ -97,6 +97,8 @@ def parse(argv=None):
     ap.add_argument('--no-legs', action='store_true', help='skip the config 3/4/5 objects of the default line')
     ap.add_argument('--train-form', choices=['auto', 'split', 'pair'], default='auto',
                     help="fs_tuning.train_form: the local-training kernel form for parallel clients (A/B runs)")
+    ap.add_argument('--split-early', choices=['auto', 'off'], default='auto',
+                    help="fs_tuning.split_early: the split form's early row issue (A/B runs)")
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
@@ -482,7 +484,8 @@ def worker(args):
     import fedamw_amd  # noqa: F401
     ws, rank, dev, dinfo = setup_rank(args)
     from fedamw_amd import _lib as flib
-    flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2}[args.train_form])
+    flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2}[args.train_form],
+                    split_early={'auto': 0, 'off': -1}[args.split_early])
     wl = {k: getattr(args, k) for k in ('algo', 'clients', 'rows', 'D', 'C', 'test', 'shape')}
     wl['config'] = args.config
     headline = (args.config == 2 and not args.custom)

@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 10
+#define FS_ABI_VERSION 11
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -69,6 +69,9 @@ const char* fs_last_error(void);
  *   train_form         (ABI 10) fs_local_train_plan's choice for parallel clients: 0 = by shape
  *                      (the pair form where it fits, else the split form), 1 = never the pair
  *                      form, 2 = the pair form wherever it fits (else as 0)
+ *   split_early        (ABI 11) split form without a prox anchor on full slices: 0 = issue the
+ *                      first 8 of each wave's next-step row loads right after the hand-off
+ *                      (they stream through the softmax), -1 = all of them inside the backward
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -90,6 +93,7 @@ typedef struct fs_tuning {
   unsigned spin_limit;
   int inject_timeout;
   int train_form;
+  int split_early;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);

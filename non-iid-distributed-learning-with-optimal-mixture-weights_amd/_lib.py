@@ -62,7 +62,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
@@ -75,7 +75,8 @@ class Tuning(C.Structure):
     """fs_tuning (include/fedsim.h), field for field: how -- never what -- the kernels compute."""
     _fields_ = [('mix_solver', C.c_int), ('mix_prefetch', C.c_int), ('mix_prefetch_lead', C.c_int),
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
-                ('inject_timeout', C.c_int), ('train_form', C.c_int)]
+                ('inject_timeout', C.c_int), ('train_form', C.c_int),
+                ('split_early', C.c_int)]
 
 
 class PlanDesc(C.Structure):

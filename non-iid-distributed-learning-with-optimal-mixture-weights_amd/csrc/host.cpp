@@ -49,6 +49,8 @@ extern "C" int fs_set_tuning(const fs_tuning* t) {
     return fs::fail(FS_EINVAL, "fs_set_tuning: mix_prefetch must be in [-1, 224], mix_prefetch_lead >= 0");
   if (t && (t->train_form < 0 || t->train_form > 2))
     return fs::fail(FS_EINVAL, "fs_set_tuning: train_form must be 0, 1 or 2");
+  if (t && (t->split_early < -1 || t->split_early > 0))
+    return fs::fail(FS_EINVAL, "fs_set_tuning: split_early must be -1 or 0");
   std::lock_guard<std::mutex> lk(fs::g_tune_m);
   fs::g_tune = t ? *t : fs_tuning{};
   return FS_OK;

@@ -47,6 +47,18 @@ constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_TPW = 2;                 // max 64-column tiles per wave (register budget)
 constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
 constexpr int SP_ERR_BYTES = 256;         // error block at the END of the workspace (never memset)
+// next-step row loads per wave issued ahead of the backward: SP_E1 right after the hand-off,
+// SP_E2 after the S2 barrier, SP_E3 after S3 (the rest inside the backward)
+#ifndef SP_E1
+#define SP_E1 6
+#endif
+#ifndef SP_E2
+#define SP_E2 0
+#endif
+#ifndef SP_E3
+#define SP_E3 0
+#endif
+constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -77,8 +89,9 @@ constexpr int SP_ERR_BYTES = 256;         // error block at the END of the works
 // Round 3: odd groups started half a step late (so half the CUs stream while the other half
 // hand off) changed nothing (configs 2 / 4 / 5 within 0.5 %): the row stream is bound per CU,
 // not by the chip's HBM.
-template <int RT, int G, bool PROX>
+template <int RT, int G, bool PROX, int EARLY>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
+  static_assert(EARLY == 0 || !PROX, "early row issue: the prox anchor's loads would queue behind it");
   constexpr int NW = SP_WAVES;
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
@@ -403,8 +416,29 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         }
         SP_STAMP(4)
       }
+      // the first SP_EARLY of this wave's next-step row loads go out here, behind the hand-off's
+      // polls (which have all returned): they stream through S2, the softmax and S3 instead of
+      // waiting for the backward (FedAvg / FedAMW on full slices; the prox anchor's loads would
+      // queue behind them)
+      constexpr int NLD = TPW * 4 * RT;           // row loads per wave and step
+      constexpr int NE = EARLY < NLD ? EARLY : NLD;
+      auto issue_row = [&](int f) {                 // (f is a constant after unrolling)
+        const int i = f / (4 * RT), kk = f % (4 * RT);
+        xf[i][kk >> 2][kk & 3] =
+            ld4(P.phi + (int64_t)pn[kk >> 2] * ld + 64 * t0 + 4 * lg + 64 * (w + NW * i) + 16 * (kk & 3));
+      };
+      // (EARLY instances run only on full slices and issue every load unconditionally -- pn
+      // always holds valid rows -- so the step is one straight path with one register
+      // assignment for xf)
+      constexpr int NE1 = SP_E1 < NE ? SP_E1 : NE, NE2 = SP_E1 + SP_E2 < NE ? SP_E1 + SP_E2 : NE;
+      if constexpr (NE > 0)
+#pragma unroll
+        for (int f = 0; f < NE1; ++f) issue_row(f);
       SP_STAMP(5)
       lds_barrier();  // S2: summed logits and norms, the image
+      if constexpr (NE > 0)
+#pragma unroll
+        for (int f = NE1; f < NE2; ++f) issue_row(f);
       SP_STAMP(6)
       const float invb = 1.0f / (float)bc;
       float cep = 0.f;
@@ -434,6 +468,9 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       cep = wave_sum_dpp(cep, lane);
       if (lane == 0) wce[w] = cep;
       lds_barrier();  // S3: g, CE partials
+      if constexpr (NE > 0)
+#pragma unroll
+        for (int f = NE2; f < NE; ++f) issue_row(f);
       SP_STAMP(7)
       const float pn2 = nrm[0], wn2 = nrm[1];
       if (g == 0 && tid == 0 && e == E - 1) {
@@ -462,7 +499,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       // load would make the compiler wait for it at the join)
       // FULL: every wave owns TPW tiles (NTS = NW * TPW, every BASELINE shape but chained config
       // 1), so no tile guard splits the block either
-      auto bwd = [&](auto LD, auto FULL) {
+      auto bwd = [&](auto LD, auto FULL, auto EA) {
+        constexpr int EAN = decltype(EA)::value;   // row loads already issued (early)
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         const int Tl = w + NW * i;
@@ -489,8 +527,15 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
             const float4 x = ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RSx);
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
-            if constexpr (decltype(LD)::value)
-              xf[i][kk >> 2][kk & 3] = ld4(P.phi + (int64_t)pn[kk >> 2] * ld + 64 * t0 + 4 * lg + 64 * Tl + 16 * (kk & 3));
+            if constexpr (decltype(LD)::value) {
+              if constexpr (EAN == 0) {
+                xf[i][kk >> 2][kk & 3] = ld4(P.phi + (int64_t)pn[kk >> 2] * ld + 64 * t0 + 4 * lg + 64 * Tl + 16 * (kk & 3));
+              } else {
+                // iteration it of the wave's backward issues load it + EAN (the rest of the
+                // stream goes out in the first NLD - EAN iterations)
+                if (i * 4 * RT + kk + EAN < NLD) issue_row(i * 4 * RT + kk + EAN);
+              }
+            }
           }
           if (l16 < C) {
 #pragma unroll
@@ -514,13 +559,16 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         }
       }
       };
-      if (ilv) {
+      using E0 = std::integral_constant<int, 0>;
+      if constexpr (NE > 0) {
+        bwd(std::true_type{}, std::true_type{}, std::integral_constant<int, NE>{});
+      } else if (ilv) {
         if (NTS == NW * TPW)
-          bwd(std::true_type{}, std::true_type{});
+          bwd(std::true_type{}, std::true_type{}, E0{});
         else
-          bwd(std::true_type{}, std::false_type{});
+          bwd(std::true_type{}, std::false_type{}, E0{});
       } else {
-        bwd(std::false_type{}, std::false_type{});
+        bwd(std::false_type{}, std::false_type{}, E0{});
       }
       if (ilv) {
         if (w == 0 && lg == 0)                     // (after the rows: nothing waits on it here)
@@ -618,18 +666,22 @@ static unsigned split_spin_limit() {
   return t.spin_limit ? t.spin_limit : SP_SPIN_LIMIT;
 }
 
-template <int RT, int G, bool PROX>
+template <int RT, int G, bool PROX, int EARLY>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
 }
 
 template <int RT, int G>
 static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (P.prox) launch_split_s<RT, G, true>(P, X, grid, lds, st);
-  else launch_split_s<RT, G, false>(P, X, grid, lds, st);
+  // early row issue where every workgroup's slice is full (NT = G * 16 tiles) and no prox
+  // anchor is re-read (fs_tuning.split_early: 0 = by shape, -1 = never)
+  const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
+  if (P.prox) launch_split_s<RT, G, true, 0>(P, X, grid, lds, st);
+  else if (full && SP_EARLY > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, SP_EARLY>(P, X, grid, lds, st);
+  else launch_split_s<RT, G, false, 0>(P, X, grid, lds, st);
 }
 
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {

@@ -1,4 +1,4 @@
-"""The pair-client form of fs_local_train (csrc/local_train_pair.hip, ABI 10).
+"""The pair-client form of fs_local_train (csrc/local_train_pair.hip, since ABI 10).
 
 A group of G workgroups trains two clients at a time, interleaved; per step it runs the
 split form's arithmetic at the same width in the same order, so the two forms must agree
