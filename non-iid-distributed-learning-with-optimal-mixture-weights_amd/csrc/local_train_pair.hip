@@ -508,16 +508,28 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
             if (PROX) gr = gr + (wc - ac) * sp;
             if (P.reg) gr = gr + wc * sr;
             o[e4] = wc - lr * gr;
-            const float dp = o[e4] - ac;
-            npn += dp * dp;
-            nwn += o[e4] * o[e4];
+            if (PROX) {                            // (without a prox term: below, if ridge)
+              const float dp = o[e4] - ac;
+              npn += dp * dp;
+              nwn += o[e4] * o[e4];
+            }
           }
           wr[YL][q] = make_float4(o[0], o[1], o[2], o[3]);
         }
       }
-      npn = wave_sum_dpp(npn, lane);
-      nwn = wave_sum_dpp(nwn, lane);
-      if (lane == 0) { wred[YL][w][0] = npn; wred[YL][w][1] = nwn; }
+      // the norms feed only the prox / ridge terms; ridge alone sums ||W||^2 here in the
+      // update's own order (q, e4: the split form's bits; padding lanes hold zeros)
+      if (!PROX && P.reg) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) nwn += comp(wr[YL][q], e4) * comp(wr[YL][q], e4);
+      }
+      if (PROX || P.reg) {
+        npn = PROX ? wave_sum_dpp(npn, lane) : 0.f;
+        nwn = wave_sum_dpp(nwn, lane);
+        if (lane == 0) { wred[YL][w][0] = npn; wred[YL][w][1] = nwn; }
+      }
       if (st == cc[YL].steps - 1) {               // client end
         if (cl) {
           float* Wj = P.W_out + (int64_t)cc[YL].j * C * ld + wbase;

@@ -549,9 +549,11 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
                 if (PROX) gr = gr + (wc - ac) * sp;
                 if (P.reg) gr = gr + wc * sr;
                 o[e4] = wc - lr * gr;
-                const float dp = o[e4] - ac;
-                npn += dp * dp;
-                nwn += o[e4] * o[e4];
+                if (PROX) {                        // (without a prox term: after the loop, if ridge)
+                  const float dp = o[e4] - ac;
+                  npn += dp * dp;
+                  nwn += o[e4] * o[e4];
+                }
               }
               wr[i][q] = make_float4(o[0], o[1], o[2], o[3]);
             }
@@ -577,9 +579,22 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         lc_ok = sp_advance(lc, P, grp, ng, T);
         if (lc_ok) fetch_rows();
       }
-      npn = wave_sum_dpp(npn, lane);
-      nwn = wave_sum_dpp(nwn, lane);
-      if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
+      // the norms of the updated slice feed only the prox / ridge terms (loss and gradient): without
+      // either nothing reads them; ridge alone sums ||W||^2 here in the update's own order (i, q,
+      // e4: the same bits as summing it inline; padding lanes and tiles hold zeros)
+      if (!PROX && P.reg) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) nwn += comp(wr[i][q], e4) * comp(wr[i][q], e4);
+      }
+      if (PROX || P.reg) {
+        npn = PROX ? wave_sum_dpp(npn, lane) : 0.f;
+        nwn = wave_sum_dpp(nwn, lane);
+        if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
+      }
       SP_STAMP(8)
     }
     if (st == cc.steps - 1) {                     // client end
