@@ -9,7 +9,7 @@
 // and walks the clients; consecutive threads read consecutive 16 B, so every client
 // row is one coalesced sweep.  When C*ld/4 threads cannot fill the chip the client
 // range is cut into `chunks` consecutive pieces folded in parallel (stage 1) and the
-// partials are folded in order (stage 2).
+// partials are folded by a fixed tree (stage 2: strided in-order sums, then those in order).
 #include "common.h"
 
 namespace fs {
@@ -51,16 +51,35 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict_
   st4(out + (int64_t)k * out_stride + 4 * i, acc);
 }
 
+// stage 2: FP_SUB threads per float4 position, thread s folding the partials k = s, s + FP_SUB,
+// ... in order, then thread 0 of the position folding the FP_SUB sums in order (a fixed tree:
+// the same bits every run).  One thread per position walking all K partials put only len4 / 256
+// workgroups on the chip (config 4: 20 CUs, 20 us for 5 MB of partials).
+constexpr int FP_SUB = 8, FP_POS = 256 / FP_SUB;
+
 __global__ __launch_bounds__(256) void fold_partials_kernel(const float* __restrict__ part, int K, int64_t len4,
                                                            float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= len4) return;
-  float4 acc = ld4(part + 4 * i);
-  for (int k = 1; k < K; ++k) {
-    const float4 v = ld4(part + (int64_t)k * 4 * len4 + 4 * i);
-    acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
+  __shared__ float4 sums[FP_SUB][FP_POS];
+  const int sub = threadIdx.x / FP_POS, pl = threadIdx.x % FP_POS;
+  const int64_t i = (int64_t)blockIdx.x * FP_POS + pl;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < len4 && sub < K) {
+    acc = ld4(part + (int64_t)sub * 4 * len4 + 4 * i);
+    for (int k = sub + FP_SUB; k < K; k += FP_SUB) {
+      const float4 v = ld4(part + (int64_t)k * 4 * len4 + 4 * i);
+      acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
+    }
   }
-  st4(out + 4 * i, acc);
+  sums[sub][pl] = acc;
+  __syncthreads();
+  if (sub == 0 && i < len4) {
+    float4 t = sums[0][pl];
+    for (int s2 = 1; s2 < FP_SUB && s2 < K; ++s2) {
+      const float4 v = sums[s2][pl];
+      t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+    }
+    st4(out + 4 * i, t);
+  }
 }
 
 }  // namespace fs
@@ -95,7 +114,8 @@ extern "C" int fs_aggregate(const float* d_W_all, int64_t stride, const float* d
   } else {
     hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)bx, chunks), dim3(256), 0, st, d_W_all, stride, d_p, N, len4,
                        per, d_ws, len);
-    hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)bx), dim3(256), 0, st, d_ws, chunks, len4, d_W_bar);
+    hipLaunchKernelGGL(fold_partials_kernel, dim3((unsigned)((len4 + FP_POS - 1) / FP_POS)), dim3(256), 0, st, d_ws,
+                       chunks, len4, d_W_bar);
   }
   FS_LAUNCH_CHECK();
   return FS_OK;
