@@ -13,7 +13,8 @@
 // new [227,396); i = 623 the new words 0 and 396); tempering is lane-parallel; the
 // Fisher-Yates swaps are inherently serial and run on lane 0 out of LDS.  Passes are
 // independent, so a round's hundreds of passes fill the chip; the replay never
-// touches the host and costs one launch per round.
+// touches the host and costs one launch per round.  Passes of at most 64 rows run one per
+// lane instead (randperm_lanes_kernel below).
 #include "common.h"
 
 namespace fs {
@@ -124,6 +125,56 @@ __global__ __launch_bounds__(RP_THREADS) void randperm_kernel(const int64_t* __r
     for (int i = lane; i < n; i += RP_THREADS) dst[i] = perm[i];
 }
 
+// Short passes (every n <= RL_MAXN, config 4's 64-row clients): one LANE per pass, 64 passes
+// per wave.  A pass of n rows draws n - 1 words, the first n - 1 of MT19937's first twist:
+// word k = mix(mt[k], mt[k+1], mt[k+397]) (k < 227 needs no word the twist rewrote first), so
+// the seeding recurrence runs to 397 + n - 2 and only mt[0..n-1] and mt[397..397+n-2] are kept
+// -- in registers, the recurrence fully unrolled (compile-time slots).  Fisher-Yates on the
+// lane's own LDS row (stride RL_MAXN + 1: the lanes' sequential accesses hit distinct banks).
+// The one-wave-per-pass form above keeps 63 of 64 lanes idle through the serial seeding and
+// swaps; next to a training launch its thousands of waves compete for the CUs.
+constexpr int RL_MAXN = 64;
+
+__global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __restrict__ seeds,
+                                                           const int64_t* __restrict__ ns,
+                                                           const int64_t* __restrict__ offs, int64_t npasses,
+                                                           int32_t* __restrict__ out) {
+  __shared__ int32_t perm_s[64][RL_MAXN + 1];
+  const int lane = threadIdx.x;
+  const int64_t pass = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = pass < npasses;
+  const int n = live ? (int)ns[pass] : 0;
+  int32_t* perm = perm_s[lane];
+  uint32_t lo[RL_MAXN], hi[RL_MAXN - 1];
+  {
+    uint32_t x = live ? (uint32_t)(uint64_t)seeds[pass] : 0u;
+    lo[0] = x;
+#pragma unroll
+    for (int i = 1; i <= MT_M + RL_MAXN - 2; ++i) {
+      x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+      if (i < RL_MAXN) lo[i] = x;
+      if (i >= MT_M) hi[i - MT_M] = x;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RL_MAXN; ++i)
+    if (i < n) perm[i] = i;
+#pragma unroll
+  for (int i = 0; i < RL_MAXN - 1; ++i) {
+    if (i < n - 1) {
+      const uint32_t r = mt_temper(mt_mix(lo[i], lo[i + 1], hi[i]));
+      const int z = (int)(r % (uint32_t)(n - i));
+      const int32_t a = perm[i];
+      perm[i] = perm[i + z];
+      perm[i + z] = a;
+    }
+  }
+  if (live) {
+    int32_t* dst = out + offs[pass];
+    for (int i = 0; i < n; ++i) dst[i] = perm[i];
+  }
+}
+
 }  // namespace fs
 
 using namespace fs;
@@ -134,6 +185,12 @@ extern "C" int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, co
   if (npasses == 0) return FS_OK;
   FS_REQUIRE(d_seeds && d_n && d_off && d_out, "null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (max_n <= RL_MAXN) {
+    hipLaunchKernelGGL(randperm_lanes_kernel, dim3((unsigned)((npasses + 63) / 64)), dim3(64), 0, st, d_seeds, d_n,
+                       d_off, npasses, d_out);
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
   const size_t lds_small = sizeof(uint32_t) * 2 * MT_N;
   const size_t lds_full = lds_small + sizeof(int32_t) * (size_t)max_n;
   if (lds_full <= 160 * 1024) {

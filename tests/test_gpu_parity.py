@@ -683,9 +683,10 @@ def test_fullsize_parallel_properties(amd):
     assert (out - W0).abs().max().item() <= 1e-6 * W0.abs().max().item()
 
 
-@pytest.mark.parametrize('n', [1, 2, 511, 512, 12800, 50000])
+@pytest.mark.parametrize('n', [1, 2, 33, 63, 64, 65, 511, 512, 12800, 50000])
 def test_device_randperm_matches_host_and_torch(amd, n):
-    """fs_randperm_device (LDS path, and the global-memory path at n=50000) == host replay == torch."""
+    """fs_randperm_device (one lane per pass up to n = 64, the one-wave LDS path, and the
+    global-memory path at n=50000) == host replay == torch."""
     dev = torch.device('cuda')
     torch.manual_seed(n)
     P = 5
@@ -700,6 +701,29 @@ def test_device_randperm_matches_host_and_torch(amd, n):
     g = torch.Generator()
     g.manual_seed(int(seeds[-1]))
     np.testing.assert_array_equal(host[-n:], torch.randperm(n, generator=g).numpy())
+
+
+def test_device_randperm_short_passes_mixed(amd):
+    """The one-lane-per-pass replay (every pass <= 64 rows) over 300 passes of mixed lengths
+    0..64 (several waves, a partial last wave, empty passes) == host replay == torch."""
+    dev = torch.device('cuda')
+    rs = np.random.RandomState(64)
+    torch.manual_seed(64)
+    P = 300
+    seeds = amd.rng.draw_pass_seeds(P)
+    ns = rs.randint(0, 65, size=P).astype(np.int64)
+    ns[:3] = [64, 0, 1]
+    offs = np.concatenate([[0], np.cumsum(ns)[:-1]]).astype(np.int64)
+    total = int(ns.sum())
+    sh = amd.engine.Shuffler(ns, offs, total, dev)
+    out = sh.run(seeds)
+    host = np.empty(total, np.int32)
+    amd.rng.randperms(seeds, ns, offs, host)
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+    for i in (0, 2, 150, P - 1):
+        g = torch.Generator()
+        g.manual_seed(int(seeds[i]))
+        np.testing.assert_array_equal(host[offs[i]:offs[i] + ns[i]], torch.randperm(int(ns[i]), generator=g).numpy())
 
 
 @pytest.mark.parametrize('N', [300, 1000])
