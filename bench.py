@@ -97,6 +97,8 @@ def parse(argv=None):
     ap.add_argument('--no-legs', action='store_true', help='skip the config 3/4/5 objects of the default line')
     ap.add_argument('--train-form', choices=['auto', 'split', 'pair'], default='auto',
                     help="fs_tuning.train_form: the local-training kernel form for parallel clients (A/B runs)")
+    ap.add_argument('--launch-timeout', type=float, default=1800.0,
+                    help='--gpus N launcher: wall-clock bound on the workers (seconds; 0 = none)')
     ap.add_argument('--split-early', choices=['auto', 'off'], default='auto',
                     help="fs_tuning.split_early: the split form's early row issue (A/B runs)")
     a = ap.parse_args(argv)
@@ -120,11 +122,17 @@ def _free_port():
     return port
 
 
-def spawn(n, cmd=None):
+def spawn(n, cmd=None, timeout=None):
     """Start n worker processes of this script (one per GPU; ``cmd`` overrides the command,
     for tests), relay rank 0's stdout, and return the exit code: 0 only if every worker
-    exited 0.  A failed worker ends the others (they would wait forever in a collective)."""
+    exited 0.  A failed worker ends the others (they would wait forever in a collective), and
+    so does the wall-clock bound ``timeout`` (seconds; default --launch-timeout): a rank hung
+    in a collective or in teardown after rank 0 printed its line must not hold the launcher
+    forever -- the workers are terminated, then killed, and the exit code is 124."""
+    if timeout is None:
+        timeout = parse().launch_timeout if cmd is None else 1800.0
     cmd = cmd or [sys.executable, '-u', os.path.abspath(__file__)] + sys.argv[1:]
+    t_start = time.time()
     port = _free_port()
     procs = []
     for r in range(n):
@@ -140,23 +148,32 @@ def spawn(n, cmd=None):
 
     th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
     th.start()
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
     rc = 0
     while any(p.poll() is None for p in procs):
         bad = [p for p in procs if p.poll() not in (None, 0)]
         if bad:
             rc = bad[0].returncode
             print('bench: worker pid %d exited %d; stopping the others' % (bad[0].pid, rc), file=sys.stderr, flush=True)
-            for p in procs:
-                if p.poll() is None:
-                    p.terminate()
-            deadline = time.time() + 20
-            for p in procs:
-                try:
-                    p.wait(timeout=max(0.1, deadline - time.time()))
-                except subprocess.TimeoutExpired:
-                    p.kill()
-                    p.wait()
+            stop_all()
             break
+        if timeout and time.time() - t_start > timeout:
+            print('bench: workers still running after the %.0f s launch timeout; stopping them' % timeout,
+                  file=sys.stderr, flush=True)
+            stop_all()
+            th.join(timeout=5)
+            return 124
         time.sleep(0.2)
     th.join(timeout=5)
     for p in procs:
@@ -231,11 +248,14 @@ def _np(x):
     return x.detach().cpu().numpy()
 
 
-def cpu_baseline(d, wl, budget, fedamw, rounds_R):
+def cpu_baseline(d, wl, budget, fedamw, rounds_R, z_rows=None):
     """The numpy oracle on this host's cores, on a bounded sample of the same workload:
     local training of as many clients as fit ~60 % of ``budget`` (whole rounds when they all
     fit), the aggregate and the test evaluation; FedAMW adds the Z GEMM on a sample of the
-    validation rows and a sample of the round's p-SGD steps.  Extrapolated to client-rounds/s."""
+    validation rows and 64 of the round's p-SGD steps on the round's own Z rows (``z_rows``:
+    the GPU's Z of the first validation rows, all N clients; random logits only if absent).
+    Extrapolated to client-rounds/s; ``extrapolation_factor`` = modelled round seconds /
+    measured seconds, ``measured`` = whether whole rounds were timed (no extrapolation)."""
     import torch
     from oracle import fedsim_oracle as O
     from threadpoolctl import threadpool_info
@@ -283,19 +303,30 @@ def cpu_baseline(d, wl, budget, fedamw, rounds_R):
         np.einsum('ncd,vd->ncv', np.stack(Ws).astype(np.float32), Xv, optimize=True)
         t_z = (time.perf_counter() - a) * (N / k) * (nv / sv)
         steps = rounds_R * ((nv + 15) // 16)
-        Zs = np.random.RandomState(0).standard_normal((N, C, 16 * 64)).astype(np.float32) * 0.1
-        yv = np.random.RandomState(1).randint(0, C, 16 * 64)
+        if z_rows is not None:             # [N, C, rows]: the round's own logits
+            Zs = np.ascontiguousarray(z_rows)
+            yv = _np(d['y_val'][:Zs.shape[2]]).astype(np.int64)
+            zsrc = 'the round\'s Z on %d validation rows' % Zs.shape[2]
+        else:
+            Zs = np.random.RandomState(0).standard_normal((N, C, 16 * 64)).astype(np.float32) * 0.1
+            yv = np.random.RandomState(1).randint(0, C, 16 * 64)
+            zsrc = 'random logits'
+        passes = max(1, 64 // ((Zs.shape[2] + 15) // 16))
+        ps = passes * ((Zs.shape[2] + 15) // 16)
         a = time.perf_counter()
-        O.mixture_solve_z(Zs, yv, np.full(N, 1.0 / N, np.float32), None, 1e-3, 1, 16)
-        t_solve = (time.perf_counter() - a) / 64 * steps
+        O.mixture_solve_z(Zs, yv, np.full(N, 1.0 / N, np.float32), None, 1e-3, passes, 16)
+        t_solve = (time.perf_counter() - a) / ps * steps
         t_round += t_z + t_solve
-        sample += ('; FedAMW: Z GEMM on %d of %d validation rows, 64 of the round\'s %d p-SGD steps (N=%d)'
-                   % (sv, nv, steps, N))
+        sample += ('; FedAMW: Z GEMM on %d of %d validation rows, %d of the round\'s %d p-SGD steps on %s (N=%d)'
+                   % (sv, nv, ps, steps, zsrc, N))
     el = time.perf_counter() - t0
     torch.set_rng_state(state)
     threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
+    whole = bool(rounds) and not fedamw
     return {'value': N / t_round, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
-            'sample': sample + ' of the numpy oracle, %.1f s, extrapolated to whole rounds' % el}
+            'measured': whole, 'extrapolation_factor': t_round / el,
+            'sample': sample + ' of the numpy oracle, %.1f s, %s' % (
+                el, 'whole rounds' if whole else 'extrapolated to whole rounds (x%.0f)' % (t_round / el))}
 
 
 def pool_validation(d, ws, dev):
@@ -461,7 +492,11 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
     if leg:
         out['fedamw'] = fedamw_leg(d, wl, dev, R_arg, fedamw_leg_rounds)
     if rank == 0 and ws == 1 and cpu_seconds > 0:
-        out['cpu_baseline'] = cpu_baseline(d, wl, cpu_seconds, fedamw, R_arg)
+        z_rows = None
+        if fedamw:                      # the round's own Z rows (all clients) for the p-SGD sample
+            mx = fed.mixture
+            z_rows = _np(mx.Z[:512].view(-1, wl['C'], mx.ldN)[:, :, :mx.N].permute(2, 1, 0))
+        out['cpu_baseline'] = cpu_baseline(d, wl, cpu_seconds, fedamw, R_arg, z_rows)
     del fed, d, Xs, ys, vl
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 11
+#define FS_ABI_VERSION 12
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -48,10 +48,17 @@ const char* fs_last_error(void);
 
 /* ------------------------------------------------------------------------- *
  * Tuning (ABI 9).  Every knob that changes HOW (never what) the kernels compute, as
- * explicit fields -- the library reads no environment variable.  Process-wide: a launch
- * reads the values current when it is enqueued.  All-zero = the defaults (what the
- * planners pick by shape).  fs_set_tuning(NULL) restores them; fs_tuning_size() is for
- * binding-layout checks.
+ * explicit fields -- the library reads no environment variable.  All-zero = the defaults
+ * (what the planners pick by shape); fs_tuning_size() is for binding-layout checks.
+ * Threading contract (ABI 12): a launch reads the tuning in effect for the HOST THREAD
+ * that enqueues it, at the moment it is enqueued (fs_local_train*, fs_plan_*, fs_mix_solve,
+ * fs_randperm_device ...; a launch already enqueued is never affected).  That is the
+ * thread's own override if fs_set_thread_tuning(t) set one, else the process-wide value of
+ * fs_set_tuning (mutex-protected; visible to every thread without an override).
+ * fs_set_tuning(NULL) restores the process-wide defaults; fs_set_thread_tuning(NULL)
+ * drops the calling thread's override; fs_get_tuning reports what the calling thread's
+ * next launch would use.  Two host threads that drive two plans with different solver or
+ * form choices therefore each set a thread override.
  *   mix_solver         0 = by shape, else force one p-solver (FS_SOLVER_*; a forced solver
  *                      that does not cover the shape falls through to the shape's choice)
  *   mix_prefetch       L2 prefetch helper workgroups beside the p-solve: 0 = by solver
@@ -70,8 +77,9 @@ const char* fs_last_error(void);
  *                      (the pair form where it fits, else the split form), 1 = never the pair
  *                      form, 2 = the pair form wherever it fits (else as 0)
  *   split_early        (ABI 11) split form without a prox anchor on full slices: 0 = issue the
- *                      first 8 of each wave's next-step row loads right after the hand-off
- *                      (they stream through the softmax), -1 = all of them inside the backward
+ *                      first SP_E1 (local_train_split.hip: 4 at G = 2, 6 at G >= 4) of each
+ *                      wave's 16 next-step row loads right after the hand-off (they stream
+ *                      through the softmax), -1 = all of them inside the backward
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -98,6 +106,7 @@ typedef struct fs_tuning {
 
 int64_t fs_tuning_size(void);
 int fs_set_tuning(const fs_tuning* t);
+int fs_set_thread_tuning(const fs_tuning* t);
 int fs_get_tuning(fs_tuning* t);
 
 /* ------------------------------------------------------------------------- *
@@ -129,10 +138,14 @@ int fs_libsvm_read(const char* path, int64_t n_rows, int64_t n_features, int zer
                    int nthreads);
 
 /* ------------------------------------------------------------------------- *
- * Device: the same shuffle replay as fs_randperm_batch, on the GPU (one wave per
- * pass; d_seeds/d_n/d_off are device arrays of npasses int64; max_n bounds n[i] and
- * selects an LDS-resident (max_n <= ~38K) or in-place global-memory permutation).
- * Bit-identical to fs_randperm_batch.  Asynchronous on `stream`.
+ * Device: the same shuffle replay as fs_randperm_batch, on the GPU; d_seeds/d_n/d_off
+ * are device arrays of npasses int64.  max_n MUST bound every n[i] (the device cannot
+ * check it before choosing the form): max_n <= 64 runs one pass per LANE (64 passes per
+ * wave, the MT state and the shuffle in registers / the lane's LDS row; a pass longer than
+ * 64 there is written as the identity permutation -- memory-safe, not torch's draw);
+ * larger max_n runs one wave per pass with an LDS-resident (max_n <= ~38K) or in-place
+ * global-memory permutation.  Bit-identical to fs_randperm_batch.  Asynchronous on
+ * `stream`.
  * ------------------------------------------------------------------------- */
 int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t* d_off, int64_t npasses,
                        int64_t max_n, int32_t* d_out, void* stream);

@@ -18,6 +18,7 @@ _SIGS = {
     'fs_last_error': (C.c_char_p, []),
     'fs_tuning_size': (C.c_int64, []),
     'fs_set_tuning': (C.c_int, [C.c_void_p]),
+    'fs_set_thread_tuning': (C.c_int, [C.c_void_p]),
     'fs_get_tuning': (C.c_int, [C.c_void_p]),
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     'fs_libsvm_scan': (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -62,7 +63,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
@@ -128,15 +129,16 @@ def lib():
 
 
 def get_tuning():
-    """The library's current fs_tuning as a dict."""
+    """The fs_tuning the calling thread's next launch would use, as a dict (include/fedsim.h:
+    the thread's own override, else the process-wide value)."""
     t = Tuning()
     check(lib().fs_get_tuning(C.byref(t)), 'fs_get_tuning')
     return {k: getattr(t, k) for k, _ in Tuning._fields_}
 
 
 def set_tuning(**fields):
-    """Set fs_tuning fields (the others keep their current values).  ``mix_solver`` may be a
-    solver name ('quad', 'qmc', ...).  Returns the previous settings (a dict)."""
+    """Set process-wide fs_tuning fields (the others keep their current values).  ``mix_solver``
+    may be a solver name ('quad', 'qmc', ...).  Returns the previous settings (a dict)."""
     prev = get_tuning()
     cur = dict(prev)
     for k, v in fields.items():
@@ -148,6 +150,23 @@ def set_tuning(**fields):
     t = Tuning(**cur)
     check(lib().fs_set_tuning(C.byref(t)), 'fs_set_tuning')
     return prev
+
+
+def set_thread_tuning(fields=None):
+    """fs_set_thread_tuning: an override for the launches the calling host thread enqueues
+    (``fields``: a dict over the process-wide defaults, solver names allowed), or None to drop
+    the thread's override."""
+    if fields is None:
+        check(lib().fs_set_thread_tuning(None), 'fs_set_thread_tuning')
+        return
+    cur = {k: 0 for k, _ in Tuning._fields_}
+    for k, v in fields.items():
+        if k not in cur:
+            raise KeyError('fs_tuning has no field %r' % k)
+        if k == 'mix_solver' and isinstance(v, str):
+            v = 0 if v == 'auto' else SOLVERS[v]
+        cur[k] = int(v)
+    check(lib().fs_set_thread_tuning(C.byref(Tuning(**cur))), 'fs_set_thread_tuning')
 
 
 class tuning:

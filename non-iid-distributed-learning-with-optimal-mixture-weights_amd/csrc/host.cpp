@@ -32,10 +32,24 @@ int fail(int code, const std::string& msg) {
 
 static std::mutex g_tune_m;
 static fs_tuning g_tune{};
+// fs_set_thread_tuning: an override for the launches this host thread enqueues
+static thread_local bool t_tune_set = false;
+static thread_local fs_tuning t_tune{};
 
 fs_tuning tuning() {
+  if (t_tune_set) return t_tune;
   std::lock_guard<std::mutex> lk(g_tune_m);
   return g_tune;
+}
+
+static int check_tuning(const fs_tuning* t, const char* fn) {
+  if (t && (t->mix_prefetch < -1 || t->mix_prefetch > 224 || t->mix_prefetch_lead < 0))
+    return fail(FS_EINVAL, std::string(fn) + ": mix_prefetch must be in [-1, 224], mix_prefetch_lead >= 0");
+  if (t && (t->train_form < 0 || t->train_form > 2))
+    return fail(FS_EINVAL, std::string(fn) + ": train_form must be 0, 1 or 2");
+  if (t && (t->split_early < -1 || t->split_early > 0))
+    return fail(FS_EINVAL, std::string(fn) + ": split_early must be -1 or 0");
+  return FS_OK;
 }
 
 }  // namespace fs
@@ -45,14 +59,16 @@ extern "C" int fs_abi_version(void) { return FS_ABI_VERSION; }
 extern "C" int64_t fs_tuning_size(void) { return (int64_t)sizeof(fs_tuning); }
 
 extern "C" int fs_set_tuning(const fs_tuning* t) {
-  if (t && (t->mix_prefetch < -1 || t->mix_prefetch > 224 || t->mix_prefetch_lead < 0))
-    return fs::fail(FS_EINVAL, "fs_set_tuning: mix_prefetch must be in [-1, 224], mix_prefetch_lead >= 0");
-  if (t && (t->train_form < 0 || t->train_form > 2))
-    return fs::fail(FS_EINVAL, "fs_set_tuning: train_form must be 0, 1 or 2");
-  if (t && (t->split_early < -1 || t->split_early > 0))
-    return fs::fail(FS_EINVAL, "fs_set_tuning: split_early must be -1 or 0");
+  if (int rc = fs::check_tuning(t, "fs_set_tuning")) return rc;
   std::lock_guard<std::mutex> lk(fs::g_tune_m);
   fs::g_tune = t ? *t : fs_tuning{};
+  return FS_OK;
+}
+
+extern "C" int fs_set_thread_tuning(const fs_tuning* t) {
+  if (int rc = fs::check_tuning(t, "fs_set_thread_tuning")) return rc;
+  fs::t_tune_set = t != nullptr;
+  fs::t_tune = t ? *t : fs_tuning{};
   return FS_OK;
 }
 

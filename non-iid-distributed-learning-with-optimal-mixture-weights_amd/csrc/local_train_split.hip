@@ -693,9 +693,13 @@ template <int RT, int G>
 static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   // early row issue where every workgroup's slice is full (NT = G * 16 tiles) and no prox
   // anchor is re-read (fs_tuning.split_early: 0 = by shape, -1 = never)
+  // Depth per width (profiles/r03/split_early_ab2.txt, launch ms): at G = 2 (128 KB of rows per
+  // CU per step) 4 early loads are fastest (config 2: 0.300-0.302 vs 0.304-0.307 with 6), at
+  // G = 16 6 (config 5: 5.34-5.36 vs 5.58 with 4)
+  constexpr int EARLY_G = (G == 2 && SP_EARLY > 4) ? 4 : SP_EARLY;
   const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
   if (P.prox) launch_split_s<RT, G, true, 0>(P, X, grid, lds, st);
-  else if (full && SP_EARLY > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, SP_EARLY>(P, X, grid, lds, st);
+  else if (full && EARLY_G > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, EARLY_G>(P, X, grid, lds, st);
   else launch_split_s<RT, G, false, 0>(P, X, grid, lds, st);
 }
 

@@ -1,10 +1,8 @@
 // FedAMW mixture-weight estimation (/root/reference/functions/tools.py:435-453).
 //
-// fs_mix_z:     Z[v][c*ldN + n] = X_val[v] . W_n[c]        -- fp32 MFMA GEMM, MFMA-bound
-//               (ldN = N rounded up to 4; the padding columns are written as zeros)
-//               (M = n_val, N = C*clients, K = D).  The reference recomputes this matmul
-//               for every 16-row batch of every inner epoch (tools.py:448); W is fixed
-//               during the p-solve, so it is computed once per round here.
+// fs_mix_z:     Z[v][c*ldN + n] = X_val[v] . W_n[c]: the fp32 MFMA GEMM in mix_z.hip
+//               (the reference recomputes this matmul for every 16-row batch of every inner
+//               epoch, tools.py:448; W is fixed during the p-solve, so once per round here).
 // fs_mix_solve: all `epochs * ceil(n_val/Bv)` dependent p-SGD steps of one round in ONE
 //               persistent workgroup (a grid-wide barrier per step would cost more than
 //               the step): out = Z_b p, CE, grad_p = Z_b^T g, momentum update.
@@ -17,71 +15,6 @@ namespace fs {
 
 // client stride of a Z row segment: N rounded up to 4 (16-byte aligned class segments)
 __host__ __device__ __forceinline__ int mix_ldn(int N) { return (N + 3) & ~3; }
-
-// ----------------------------------------------------------------------------
-// Z GEMM: 64 x 64 output tile per 256-thread workgroup, BK = 16, LDS-staged,
-// each wave a 32 x 32 quadrant = 2 x 2 tiles of v_mfma_f32_16x16x4_f32.
-// ----------------------------------------------------------------------------
-constexpr int MZ_BM = 64, MZ_BN = 64, MZ_BK = 16, MZ_PAD = 4;
-
-__global__ __launch_bounds__(256) void mix_z_kernel(const float* __restrict__ W, const float* __restrict__ X,
-                                                   int64_t ld, int N, int C, int nv, float* __restrict__ Z) {
-  __shared__ float As[MZ_BM][MZ_BK + MZ_PAD];
-  __shared__ float Bs[MZ_BN][MZ_BK + MZ_PAD];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
-  const int ldN = mix_ldn(N);
-  const int CN = C * ldN;                          // padded columns: c * ldN + n, n < ldN
-  const int v0 = blockIdx.y * MZ_BM;
-  const int c0 = blockIdx.x * MZ_BN;
-  // loader mapping: thread -> (row, 4-float group) of a 64 x 16 tile
-  const int lr = tid >> 2, lk = (tid & 3) * 4;
-  const int va = v0 + lr;
-  const float* arow = va < nv ? X + (int64_t)va * ld : nullptr;
-  const int cb = c0 + lr;
-  const float* brow = nullptr;
-  if (cb < CN) {
-    const int c = cb / ldN, n = cb - c * ldN;
-    if (n < N) brow = W + ((int64_t)n * C + c) * ld;   // padding clients: zero columns
-  }
-  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
-  floatx4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t k0 = 0; k0 < ld; k0 += MZ_BK) {
-    const float4 av = arow ? ld4(arow + k0 + lk) : zero4;
-    const float4 bv = brow ? ld4(brow + k0 + lk) : zero4;
-    __syncthreads();
-    st4(&As[lr][lk], av);
-    st4(&Bs[lr][lk], bv);
-    __syncthreads();
-#pragma unroll
-    for (int kq = 0; kq < MZ_BK / 4; ++kq) {
-      float a[2], b[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        a[t] = As[wr + 16 * t + l16][4 * kq + lg];
-        b[t] = Bs[wc + 16 * t + l16][4 * kq + lg];
-      }
-#pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = mfma4(a[ti], b[tj], acc[ti][tj]);
-    }
-  }
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int v = v0 + wr + 16 * ti + 4 * lg + i;
-        const int col = c0 + wc + 16 * tj + l16;
-        if (v < nv && col < CN) Z[(int64_t)v * CN + col] = acc[ti][tj][i];
-      }
-}
 
 // ----------------------------------------------------------------------------
 // p-solve: one workgroup of 1024 threads.  p and the momentum buffer live in LDS.
@@ -2013,19 +1946,6 @@ extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   const int nk = qmc_nk(C);
   const int64_t qmc = mc_xbytes((mix_ldn(N) + 16 * nk - 1) / (16 * nk));
   return std::max(mc, (N > 128 && C <= 16 && Bv <= 16) ? qmc : (int64_t)0) + MC_ERR_BYTES;
-}
-
-extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, int N, int C, int n_val, float* d_Z,
-                        void* stream) {
-  FS_REQUIRE(N >= 1 && C >= 1 && n_val >= 1, "bad sizes");
-  FS_REQUIRE(ld >= 64 && ld % 64 == 0, "ld must be a positive multiple of 64");
-  FS_REQUIRE(d_W_all && d_X_val && d_Z, "null pointer");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int CN = C * mix_ldn(N);                  // padded columns (zeros for n >= N)
-  dim3 grid((CN + MZ_BN - 1) / MZ_BN, (n_val + MZ_BM - 1) / MZ_BM);
-  hipLaunchKernelGGL(mix_z_kernel, grid, dim3(256), 0, st, d_W_all, d_X_val, ld, N, C, n_val, d_Z);
-  FS_LAUNCH_CHECK();
-  return FS_OK;
 }
 
 extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,

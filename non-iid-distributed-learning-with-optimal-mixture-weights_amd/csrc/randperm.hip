@@ -143,7 +143,11 @@ __global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __res
   const int lane = threadIdx.x;
   const int64_t pass = (int64_t)blockIdx.x * 64 + lane;
   const bool live = pass < npasses;
-  const int n = live ? (int)ns[pass] : 0;
+  const int n_req = live ? (int)ns[pass] : 0;
+  // the contract (fedsim.h): every ns[pass] <= max_n; this form is chosen for max_n <= RL_MAXN.
+  // A longer pass (a caller bug) must not shuffle into its neighbours' LDS rows: it is written
+  // as the identity permutation -- valid row indices, memory-safe, and not torch's draw
+  const int n = n_req <= RL_MAXN ? n_req : 0;
   int32_t* perm = perm_s[lane];
   uint32_t lo[RL_MAXN], hi[RL_MAXN - 1];
   {
@@ -172,6 +176,7 @@ __global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __res
   if (live) {
     int32_t* dst = out + offs[pass];
     for (int i = 0; i < n; ++i) dst[i] = perm[i];
+    for (int i = n; i < n_req; ++i) dst[i] = i;
   }
 }
 

@@ -193,7 +193,7 @@ def mixture_solve_z(Z, yv, p, buf, lr_p, epochs, batch_size=16, momentum=0.9):
     """The p-SGD of ``mixture_solve`` on precomputed validation logits Z [N, C, n_v]
     (tools.py:448 with the inner matmul hoisted, Q7) -- lets a check at large N x D feed the
     GPU's own Z (itself checked separately) instead of recomputing the D-wide GEMM here."""
-    Z = np.asarray(Z, dtype=F32)
+    Zt = np.ascontiguousarray(np.asarray(Z, dtype=F32).transpose(2, 0, 1))   # [n_v, N, C]: batch rows gather whole
     yv = np.asarray(yv, dtype=np.int64)
     p = np.array(p, dtype=F32, copy=True)
     lr32, mom32 = F32(lr_p), F32(momentum)
@@ -203,13 +203,13 @@ def mixture_solve_z(Z, yv, p, buf, lr_p, epochs, batch_size=16, momentum=0.9):
         for b0 in range(0, nv, batch_size):
             idx = order[b0:b0 + batch_size]
             bsz = len(idx)
-            zb = Z[:, :, idx]                       # [N, C, b]
-            out = np.einsum('ncb,n->bc', zb, p).astype(F32)
+            zb = Zt[idx]                            # [b, N, C]
+            out = np.einsum('bnc,n->bc', zb, p).astype(F32)
             logp = _log_softmax(out)
             g = np.exp(logp).astype(F32)
             g[np.arange(bsz), yv[idx]] -= F32(1.0)
             g /= F32(bsz)
-            gp = np.einsum('bc,ncb->n', g, zb).astype(F32)
+            gp = np.einsum('bc,bnc->n', g, zb).astype(F32)
             buf = gp.copy() if buf is None else (mom32 * buf + gp).astype(F32)
             p = (p - lr32 * buf).astype(F32)
     return p, buf

@@ -435,6 +435,68 @@ def run_bench(modes=('seq', 'par')):
               np.round(ta.numpy()[BENCH_SNAP], 2), 'p range', float(rec['p'].min()), float(rec['p'].max()))
 
 
+HORIZON = {
+    # config 5's solver (qmc, N > 256): N = 300 clients, C = 10, n_v >= 1,000, R = 20 ->
+    # R * ceil(n_v / 16) >= 1,200 dependent momentum steps per round, 20 rounds.  lr_p = 3e-4:
+    # at the configs' 1e-3 the reference's own p-SGD diverges to NaN here in chained mode (at
+    # local lr 0.05 .. 0.5 alike; 300 similar client models make the p-Hessian ~N times a single
+    # model's), where no fp32 restatement can follow it
+    'qmc': dict(data=dict(seed=51, n_test=200, n_raw=12, D=32, C=10, val_frac=0.2), N=300, size_range=(20, 31),
+                hp=dict(lr=0.2, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=20, lr_p=3e-4)),
+    # config 1's solver (bin: N <= 16, C = 2) at config 1's shape: 10 label-skewed clients over
+    # a9a's 32,561 rows (n_v ~ 6,500), R = 10 -> >= 4,000 steps per round
+    'bin': dict(data=dict(seed=52, n_test=300, n_raw=16, D=32, C=2, val_frac=0.2), N=10, total=32561,
+                hp=dict(lr=0.5, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-5, R=10, lr_p=1e-3)),
+}
+
+
+def horizon_sizes(name):
+    h = HORIZON[name]
+    rs = np.random.RandomState(h['data']['seed'] + 1000)
+    if 'size_range' in h:
+        return [int(v) for v in rs.randint(h['size_range'][0], h['size_range'][1], size=h['N'])]
+    w = rs.dirichlet(np.full(h['N'], 0.5))
+    s = np.maximum(100, np.floor(w * h['total'])).astype(int)
+    s[np.argmax(s)] += h['total'] - s.sum()
+    return [int(v) for v in s]
+
+
+def run_horizon(names=('qmc', 'bin'), modes=('seq', 'par')):
+    """FedAMW at the benchmarked horizons of the two p-solvers the BASELINE configs run beyond
+    config 2 (tools.py:423 momentum persisting over rounds, 441-453 the p-SGD): ``qmc`` (config
+    5's multi-CU solver, N > 256) and ``bin`` (config 1's two-class solver), chained and parallel
+    clients, p after every round, the global model after every round."""
+    torch.set_num_threads(1)
+    for name in names:
+        h = HORIZON[name]
+        d = synth(sizes=horizon_sizes(name), **h['data'])
+        nv = len(d['y_val'])
+        hp = h['hp']
+        steps = hp['R'] * ((nv + 15) // 16)
+        C, D = h['data']['C'], h['data']['D']
+        np.savez_compressed(os.path.join(OUT, 'horizon_%s_data.npz' % name), **d, torch_seed=TORCH_SEED, C=C, D=D)
+        Xs, ys, Xt, yt = _split(d)
+        vl = torch.utils.data.DataLoader(
+            torch.utils.data.TensorDataset(torch.from_numpy(d['X_val']), torch.from_numpy(d['y_val'])),
+            batch_size=16, shuffle=True)
+        pos = ('classification', C, D, hp['lr'], hp['epoch'], hp['batch_size'], hp['prox'], hp['mu'], hp['reg'],
+               hp['lam'], hp['R'])
+        for mode in modes:
+            _trace['W'].clear()
+            _trace['p'].clear()
+            torch.manual_seed(TORCH_SEED)
+            with contextlib.redirect_stdout(io.StringIO()):
+                tr, tl, ta = {'seq': T.FedAMW, 'par': _fedamw_par}[mode](Xs, ys, Xt, yt, vl, *pos, hp['lr_p'])
+            rec = {k: np.asarray(v) for k, v in hp.items()}
+            rec.update(algo='fedamw', mode=mode, solver=name, train_loss=tr.detach().numpy(), test_loss=tl.numpy(),
+                       test_acc=ta.numpy(), W=np.stack(_trace['W']), p=np.stack(_trace['p']), n_val=nv,
+                       steps_per_round=steps, rng_after=torch.empty(4, dtype=torch.int64).random_().numpy())
+            np.savez_compressed(os.path.join(OUT, 'horizon_%s_%s.npz' % (name, mode)), **rec)
+            print('horizon', name, mode, 'N', len(ys), 'n_val', nv, 'steps/round', steps, 'acc',
+                  np.round(ta.numpy()[[0, -1]], 2), 'p range', float(rec['p'].min()), float(rec['p'].max()),
+                  'finite', bool(np.isfinite(rec['p']).all()), flush=True)
+
+
 def _reference_utils():
     """Import /root/reference/functions/utils.py with the two stand-ins described above."""
     import types
@@ -629,7 +691,7 @@ def run_exp():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params', 'long', 'prep', 'bench', 'exp']
+    which = sys.argv[1:] or ['rounds', 'single', 'rff', 'params', 'long', 'prep', 'bench', 'exp', 'horizon']
     if 'bench' in which:
         run_bench()
     for m in ('seq', 'par'):
@@ -637,6 +699,12 @@ if __name__ == '__main__':
             run_bench((m,))
     if 'exp' in which:
         run_exp()
+    if 'horizon' in which:
+        run_horizon()
+    for h in HORIZON:
+        for m in ('seq', 'par'):
+            if 'horizon:%s:%s' % (h, m) in which:
+                run_horizon((h,), (m,))
     if 'long' in which:
         run_long()
     if 'prep' in which:

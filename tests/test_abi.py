@@ -62,3 +62,40 @@ def test_workspace_sizes_are_host_only():
     assert L.fs_mix_solve_ws_bytes(100, 10, 16) >= _lib.ERR_BLOCK
     assert L.fs_mix_solve_ws_bytes(1000, 10, 16) > L.fs_mix_solve_ws_bytes(10, 2, 16)   # multi-CU granules
     assert L.fs_mix_solve_last_mode() in _lib.SOLVER_NAMES
+
+
+def test_tuning_threading_contract():
+    """include/fedsim.h (ABI 12): a launch reads the tuning of the host thread that enqueues it
+    -- the thread's fs_set_thread_tuning override, else the process-wide fs_set_tuning value.
+    Checked through fs_get_tuning (what the calling thread's next launch would use); host-only."""
+    import threading
+    prev = _lib.set_tuning(mix_solver='quad')
+    try:
+        seen = {}
+
+        def worker(name, fields):
+            if fields is not None:
+                _lib.set_thread_tuning(fields)
+            seen[name + '_own'] = _lib.get_tuning()['mix_solver']
+            barrier.wait()                  # both threads hold their settings at once
+            seen[name + '_after'] = _lib.get_tuning()['mix_solver']
+            _lib.set_thread_tuning(None)
+            seen[name + '_dropped'] = _lib.get_tuning()['mix_solver']
+
+        barrier = threading.Barrier(2)
+        ts = [threading.Thread(target=worker, args=('a', {'mix_solver': 'qmc'})),
+              threading.Thread(target=worker, args=('b', None))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert seen['a_own'] == seen['a_after'] == _lib.SOLVERS['qmc']
+        assert seen['b_own'] == seen['b_after'] == _lib.SOLVERS['quad']       # the process-wide value
+        assert seen['a_dropped'] == seen['b_dropped'] == _lib.SOLVERS['quad']
+        assert _lib.get_tuning()['mix_solver'] == _lib.SOLVERS['quad']       # this thread: untouched
+        L = _lib.lib()
+        bad = _lib.Tuning(train_form=7)
+        assert L.fs_set_thread_tuning(ctypes.byref(bad)) == -1
+        assert 'train_form' in L.fs_last_error().decode()
+    finally:
+        _lib.set_tuning(**prev)

@@ -49,6 +49,19 @@ def test_spawn_stops_the_others(tmp_path):
     assert bench.spawn(2, [sys.executable, str(w)]) == 5
 
 
+def test_spawn_launch_timeout(tmp_path, capfd):
+    """A rank that never exits (here: sleeps after a clean rank 0 has printed its line and
+    exited 0) is stopped at the launcher's wall-clock bound, and the launch fails (124)."""
+    w = tmp_path / 'w.py'
+    w.write_text('import os, sys, time\nif os.environ["RANK"] == "0":\n    print("{}", flush=True)\n    sys.exit(0)\n'
+                 'time.sleep(600)\n')
+    import time
+    t0 = time.time()
+    assert bench.spawn(2, [sys.executable, str(w)], timeout=3.0) == 124
+    assert time.time() - t0 < 60
+    assert '{}' in capfd.readouterr().out
+
+
 def test_gpus_must_match_world_size(monkeypatch):
     monkeypatch.setenv('WORLD_SIZE', '2')
     args = bench.parse(['--gpus', '4'])

@@ -113,6 +113,36 @@ def test_pair_planner_and_train_form(amd):
     assert g == 4 | P and ws > amd.lib.ERR_BLOCK
 
 
+@pytest.mark.parametrize('G', [2, 4])
+@pytest.mark.parametrize('B', [32, 16])
+def test_pair_c14_boundary(amd, G, B):
+    """C = 14, the widest the pair form takes: the last real class (13) sits beside the two
+    granules that carry ||W - W_a||^2 and ||W||^2 (row 0, classes 14 and 15), with the prox and
+    ridge terms on (both norms read).  Bitwise the split form, a client against the oracle; the
+    planner never gives the pair form at C = 15 (not even when asked for it)."""
+    import ctypes
+    rs = np.random.RandomState(140 + G + B)
+    D, C, E = 512 * G, 14, 2
+    sizes = [70, 33, 1, 64, 17]
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    lr, mu, lam = 0.4, 0.03, 0.002
+    Wp, lp = _train_via_abi(amd, Xs, ys, W0, lr, E, B, True, mu, True, lam, False, seed=5, split=_pair(amd, G))
+    assert _train_via_abi.last_G == _pair(amd, G)
+    Ws, ls = _train_via_abi(amd, Xs, ys, W0, lr, E, B, True, mu, True, lam, False, seed=5, split=G)
+    assert np.array_equal(Wp, Ws), np.abs(Wp - Ws).max()
+    assert np.array_equal(lp, ls)
+    torch.manual_seed(5)
+    Wr, lref = O.train_client(Xs[0], ys[0], W0, lr, E, B, True, mu, True, lam)
+    assert np.abs(Wp[0] - Wr).max() <= 2e-5 * max(1.0, np.abs(Wr).max())
+    assert abs(lp[0] - lref) <= 2e-5 * max(1.0, abs(lref))
+    L = amd.lib.lib()
+    for want in (0, _pair(amd, G)):
+        g, w = ctypes.c_int(want), ctypes.c_int64(0)
+        amd.lib.check(L.fs_local_train_plan(1250, 15, B, 2, D, 1024, 0, 1, ctypes.byref(g), ctypes.byref(w)), 'plan')
+        assert not (g.value & amd.lib.G_PAIR), (want, g.value)
+
+
 def test_pair_handoff_timeout_raises(amd):
     """fs_tuning.inject_timeout: the pair launch reports a timeout through its workspace error
     word; check_errors raises and clears it, and the next launch is clean."""

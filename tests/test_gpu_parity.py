@@ -8,8 +8,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (BENCH_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol,
-                            load, load_bench, load_long, positional, split_clients)
+from tests.fixtures import (BENCH_CASES, HORIZON_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS,
+                            W_RTOL, acc_tol, horizon_rtol, load, load_bench, load_horizon, load_long, positional, split_clients)
 
 pytestmark = pytest.mark.gpu
 
@@ -104,6 +104,68 @@ def test_dropin_benchmark_length_fedamw(amd, name):
                                atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
     assert np.abs(ta.numpy() - d['test_acc']).max() <= acc_tol(d)
     np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['rng_after'])
+
+
+@pytest.mark.parametrize('name', HORIZON_CASES)
+def test_dropin_solver_horizon_fedamw(amd, name):
+    """The FedAMW drop-in against the reference at the horizons of the two p-solvers configs 1
+    and 5 run (tools.py:423 -- momentum persisting across rounds -- and 441-453): ``qmc``, the
+    multi-CU solver of config 5 (N = 300 > 256, C = 10, R = 20 rounds of >= 1,200 dependent
+    momentum steps, lr_p = 1e-3 as in the configs) and ``bin``, config 1's two-class solver
+    (N = 10, C = 2, n_v = 6,509: 4,070 steps per round, R = 10); chained and parallel clients.
+    Every round's global model and mixture weights, the losses, the accuracy and where the
+    generator is left."""
+    d = load_horizon(name)
+    (tr, tl, ta), stats = run_dropin(amd, d)
+    assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == str(d['solver'])
+    W = stats['W_rounds']
+    assert W.shape == d['W'].shape
+    tol = horizon_rtol(name)              # (tests/fixtures.py: 3e-5 for the chained qmc case)
+    for t in range(len(W)):
+        err = np.abs(W[t] - d['W'][t]).max()
+        assert err <= tol * np.abs(d['W'][t]).max(), (name, t, err)
+    p = stats['p'].cpu().numpy()
+    assert np.abs(p - d['p'][-1]).max() <= tol * np.abs(d['p'][-1]).max()
+    np.testing.assert_allclose(tr.numpy(), d['train_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl.numpy(), d['test_loss'], rtol=0,
+                               atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta.numpy() - d['test_acc']).max() <= acc_tol(d)
+    np.testing.assert_array_equal(torch.empty(4, dtype=torch.int64).random_().numpy(), d['rng_after'])
+
+
+def test_mix_solve_config5_horizon_vs_oracle(amd):
+    """Config 5's p-solve shape (N = 1000, C = 10; the auto choice is qmc) over R = 100 inner
+    epochs of n_val = 3,200 rows: 20,000 dependent momentum steps in one launch, lr_p = 1e-3
+    (the configs' value), against the oracle's fp32 p-SGD on the GPU's own Z (tools.py:441-453);
+    then a second call of 5,000 steps continuing p and the momentum buffer (tools.py:423)."""
+    N, C, D, nv, R = 1000, 10, 64, 3200, 100
+    rs = np.random.RandomState(17)
+    dev = torch.device('cuda')
+    Xv = (np.cos(rs.normal(size=(nv, D)) * 2.0) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=nv).astype(np.int64)
+    # logits of std ~0.35: well-conditioned (the fp32 oracle against itself with fp64
+    # accumulation of the logits and the gradient: 8e-7 of max|p| after 20,000 steps; at std 1.4
+    # that summation-order sensitivity is 4.6e-6) while p still moves by 150x its start
+    Wc = (rs.normal(size=(N, C, D)) * 0.5).astype(np.float32)
+    p0 = np.full(N, 1.0 / N, np.float32)
+    mix = amd.engine.Mixture(torch.from_numpy(Xv), torch.from_numpy(yv), D, C, N, 16, torch.from_numpy(p0), dev)
+    Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+    Wd[:, :, :D] = torch.from_numpy(Wc)
+    pr, br = p0, None
+    for call, epochs in enumerate((R, R // 4)):
+        torch.manual_seed(90 + call)
+        mix.solve(Wd, amd.rng.draw_pass_seeds(epochs), 1e-3, z=(call == 0))
+        torch.cuda.synchronize()
+        assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
+        mix.check_errors()
+        Zn = mix.Z.view(nv, C, mix.ldN)[:, :, :N].permute(2, 1, 0).contiguous().cpu().numpy()
+        torch.manual_seed(90 + call)
+        pr, br = O.mixture_solve_z(Zn, yv, pr, br, 1e-3, epochs, 16)
+        p, b = mix.p.cpu().numpy(), mix.buf.cpu().numpy()
+        assert np.abs(p - pr).max() <= P_RTOL * np.abs(pr).max(), (call, np.abs(p - pr).max(), np.abs(pr).max())
+        assert np.abs(b - br).max() <= 1e-4 * np.abs(br).max(), call
+        assert np.abs(pr - p0).max() > 10 * P_RTOL * np.abs(pr).max()      # p moved: not a vacuous check
 
 
 @pytest.mark.parametrize('chunk', [1, 3, 7])
@@ -598,6 +660,34 @@ def test_mix_solve_forced_fallbacks(amd, solver, N, C):
     with amd.lib.tuning(mix_solver=solver):
         test_mix_solve_variants(amd, N, C, 133, 16, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == solver
+
+
+@pytest.mark.parametrize('N,C,D,nv', [(1, 1, 64, 1), (3, 2, 64, 255), (23, 5, 192, 257), (100, 10, 2048, 700),
+                                      (130, 7, 320, 513), (300, 4, 128, 1000)])
+def test_mix_z_shapes(amd, N, C, D, nv):
+    """fs_mix_z (mix_z.hip: 256 x 128 tiles, K-steps of 32, LDS-DMA images) against fp64 on
+    ragged shapes: row tails (n_val mod 256), column tails (C * ldN mod 128), padding clients
+    (N mod 4), the shortest K (ld = 64: one loop iteration); padding columns exactly 0 and
+    nothing written past Z (a guard row after it)."""
+    rs = np.random.RandomState(N + nv)
+    ld = (D + 63) // 64 * 64
+    ldN = (N + 3) // 4 * 4
+    dev = torch.device('cuda')
+    X = torch.zeros(nv, ld, device=dev)
+    X[:, :D] = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
+    W = torch.zeros(N, C, ld, device=dev)
+    W[:, :, :D] = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.3).astype(np.float32))
+    Zb = torch.full((nv + 1, C * ldN), 7.0, device=dev)
+    L = amd.lib
+    L.check(L.lib().fs_mix_z(L.ptr(W), L.ptr(X), ld, N, C, nv, L.ptr(Zb), L.stream_ptr()), 'fs_mix_z')
+    torch.cuda.synchronize()
+    Z = Zb[:nv].view(nv, C, ldN).double().cpu().numpy()
+    Xd, Wd = X[:, :D].double().cpu().numpy(), W[:, :, :D].double().cpu().numpy()
+    ref = np.einsum('vd,ncd->vcn', Xd, Wd)
+    scale = np.einsum('vd,ncd->vcn', np.abs(Xd), np.abs(Wd))
+    assert (np.abs(Z[:, :, :N] - ref) <= 2e-6 * scale + 1e-30).all()
+    assert (Z[:, :, N:] == 0).all()
+    assert (Zb[nv] == 7.0).all()
 
 
 def test_mix_z_and_solve_vs_oracle(amd):

@@ -4,8 +4,8 @@ import pytest
 import torch
 
 from oracle import fedsim_oracle as O
-from tests.fixtures import (BENCH_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS, W_RTOL, acc_tol,
-                            load, load_bench, load_long, positional, split_clients)
+from tests.fixtures import (BENCH_CASES, HORIZON_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS,
+                            W_RTOL, acc_tol, horizon_rtol, load, load_bench, load_horizon, load_long, positional, split_clients)
 
 
 def run_oracle(d):
@@ -97,6 +97,24 @@ def test_benchmark_length_fedamw_matches_reference(name):
         assert np.abs(trace['W'][t] - d['W'][k]).max() <= W_RTOL * np.abs(d['W'][k]).max(), (name, t)
     for t in range(len(d['p'])):
         assert np.abs(trace['p'][t] - d['p'][t]).max() <= P_RTOL * np.abs(d['p'][t]).max(), (name, t)
+    np.testing.assert_allclose(tr, d['train_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
+    np.testing.assert_allclose(tl, d['test_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
+    assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)
+
+
+@pytest.mark.parametrize('name', HORIZON_CASES)
+def test_solver_horizon_fedamw_matches_reference(name):
+    """FedAMW at the horizons of config 5's (qmc: N = 300, C = 10, R = 20, >= 1,200 steps per
+    round) and config 1's (bin: N = 10, C = 2, 4,070 steps per round, R = 10) p-solvers: the
+    restatement against the reference, p and W after every round."""
+    d = load_horizon(name)
+    assert int(d['steps_per_round']) == int(d['R']) * ((int(d['n_val']) + 15) // 16) >= 1200
+    tr, tl, ta, trace = run_oracle(d)
+    tol = horizon_rtol(name)              # (tests/fixtures.py: 3e-5 for the chained qmc case)
+    for t in range(len(d['W'])):
+        assert np.abs(trace['W'][t] - d['W'][t]).max() <= tol * np.abs(d['W'][t]).max(), (name, t)
+    for t in range(len(d['p'])):
+        assert np.abs(trace['p'][t] - d['p'][t]).max() <= tol * np.abs(d['p'][t]).max(), (name, t)
     np.testing.assert_allclose(tr, d['train_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['train_loss']).max()))
     np.testing.assert_allclose(tl, d['test_loss'], rtol=0, atol=LOSS_RTOL * max(1, np.abs(d['test_loss']).max()))
     assert np.abs(ta - d['test_acc']).max() <= acc_tol(d)
