@@ -253,6 +253,23 @@ int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_per
                  int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
                  int* d_first, void* d_ws, int64_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * (ABI 12) fs_mix_solve on the rank-blocked Z that one all-gather of the per-rank
+ * Z blocks produces (the sharded FedAMW round, dist.py): d_Z is
+ * [blocks][n_val][C][L], L = N / blocks (a multiple of 4), client n = block n / L,
+ * column n % L -- no layout copy into [n_val][C][N] first.  Read by the qmc solver
+ * only (N > 256, C <= 16, Bv <= 16; fs_tuning.mix_solver AUTO or QMC); any other
+ * shape or forced solver returns FS_EUNSUPPORTED (use fs_mix_solve on the standard
+ * layout).  Same arithmetic in the same order as fs_mix_solve on the standard layout:
+ * bitwise the same p and momentum buffer.  Arguments otherwise as fs_mix_solve.
+ * fs_mix_solve_blocked_covers tells, before the all-gather, which layout to assemble.
+ * ------------------------------------------------------------------------- */
+int fs_mix_solve_blocked(const float* d_Z, int blocks, const int32_t* d_labels, const int32_t* d_perms, int N,
+                         int C, int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
+                         int* d_first, void* d_ws, int64_t ws_bytes, void* stream);
+/* host-only: 1 if fs_mix_solve_blocked covers this shape under the calling thread's tuning */
+int fs_mix_solve_blocked_covers(int N, int C, int n_val, int epochs, int Bv);
+
 /* Diagnostic (host state only): the solver the calling thread's last fs_mix_solve
  * launched -- FS_SOLVER_REG (1, register-resident, one row per wave), _MC (2, multi-CU),
  * _STAGED (3), _GLOBAL (4), _REG2 (5, two rows per wave, Bv <= 16, C <= 10), _WAVE (6, one

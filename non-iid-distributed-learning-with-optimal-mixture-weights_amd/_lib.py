@@ -42,6 +42,10 @@ _SIGS = {
     'fs_mix_solve': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_int64, C.c_void_p]),
+    'fs_mix_solve_blocked': (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_int, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int64, C.c_void_p]),
+    'fs_mix_solve_blocked_covers': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     'fs_mix_solve_last_mode': (C.c_int, []),
     'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                  C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),

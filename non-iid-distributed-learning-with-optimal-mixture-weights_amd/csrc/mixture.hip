@@ -312,17 +312,29 @@ constexpr int MR_WAVES = 16;
 // skips to the solver's position; it exits once the solver's count reaches the total.
 // ----------------------------------------------------------------------------
 constexpr int PF_SPIN_LIMIT = 1 << 22;
+constexpr int PF_INFLIGHT = 32;                   // 1-KB pieces a helper wave keeps in flight
 
-__device__ __noinline__ void mix_prefetch_helper(const float* __restrict__ Z, const int32_t* __restrict__ perms,
+__device__ __forceinline__ void mix_prefetch_helper(const float* __restrict__ Z, const int32_t* __restrict__ perms,
                                                  int N, int C, int nv, int epochs, int Bv, int h, int H, int lead,
-                                                 const unsigned* prog) {
+                                                 const unsigned* prog, int zL = 0, int zR = 1) {
+  // The loads only warm the caches: each is an LDS-DMA (global_load_lds_dwordx4, 1 KB per
+  // wave instruction) into a sink no one reads, so a wave needs no registers for them and
+  // keeps PF_INFLIGHT pieces in flight (a counted vmcnt throttle) instead of waiting for every
+  // 4 KB (round 3's register form: at config 5's 40-KB rows, 10 dependent round trips per row,
+  // ~5 us per step over 16 helpers -- slower than the solver, so the helpers fell behind)
+  __shared__ __attribute__((aligned(1024))) char pf_sink[1024];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nw = blockDim.x >> 6;
-  const int CN4 = C * mix_ldn(N) / 4;             // float4 per Z row (ldN % 4 == 0)
+  // Z rows: zR blocks of zL clients (fs_mix_solve_blocked: [zR][n_val][C][zL]; else one block
+  // of ldN): a row is zR segments of C * zL floats, nv * C * zL floats apart
+  if (zL == 0) zL = mix_ldn(N);
+  const int CN4 = C * zL / 4;                     // float4 per row segment (zL % 4 == 0)
+  const int64_t bstride = (int64_t)nv * C * zL;
   const int nbat = (nv + Bv - 1) / Bv;
   const int total = epochs * nbat;
   unsigned seen = 0;
+  int issued = 0;
   for (int t = h; t < total; t += H) {
     int spins = 0;
     while ((unsigned)t >= seen + (unsigned)lead) {   // pace: at most `lead` steps ahead
@@ -338,18 +350,21 @@ __device__ __noinline__ void mix_prefetch_helper(const float* __restrict__ Z, co
     }
     const int ep = t / nbat, sb = t - ep * nbat;
     const int bc = min(Bv, nv - sb * Bv);
-    for (int r = w; r < bc; r += nw) {
-      const int row = perms[(int64_t)ep * nv + sb * Bv + r];
-      const float4* zr = reinterpret_cast<const float4*>(Z + (int64_t)row * (4 * CN4));
-      for (int i0 = 0; i0 < CN4; i0 += 256) {    // 4 loads in flight per lane
-        float4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = zr[min(i0 + 64 * k + lane, CN4 - 1)];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) asm volatile("" ::"v"(v[k].x));   // keep the loads
+    for (int r = w; r < bc * zR; r += nw) {
+      const int rb = r / zR, blk = r - rb * zR;
+      const int row = __builtin_amdgcn_readfirstlane(perms[(int64_t)ep * nv + sb * Bv + rb]);
+      const float4* zr = reinterpret_cast<const float4*>(Z + blk * bstride + (int64_t)row * (4 * CN4));
+      for (int i0 = 0; i0 < CN4; i0 += 64) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(zr + min(i0 + lane, CN4 - 1)),
+                                         (__attribute__((address_space(3))) void*)pf_sink, 16, 0, 0);
+        if (++issued == PF_INFLIGHT) {
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          issued = 16;
+        }
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // the solver's side: publish the number of completed steps (vector store, relaxed agent scope)
@@ -1693,14 +1708,15 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
     int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
     int* __restrict__ first_flag, int z_bytes, unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err,
-    int K, unsigned spin_limit, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead) {
+    int K, unsigned spin_limit, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead, int zL, int zR) {
   static_assert(NK == 4 || NK == 8, "clients per lane");
   static_assert(CL >= 1 && CL <= 16, "classes");
   static_assert(DEPTH * (CL * NK / 4 + 2) <= 63, "ring vs the vmcnt window");
   if (blockIdx.x % MC_XCDS) return;
   const int bk = blockIdx.x / MC_XCDS;
   if (bk >= K) {                                   // L2 prefetch helpers on the solvers' XCD
-    if (pf_prog && bk - K < pf_h) mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, bk - K, pf_h, pf_lead, pf_prog);
+    if (pf_prog && bk - K < pf_h)
+      mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, bk - K, pf_h, pf_lead, pf_prog, zL, zR);
     return;
   }
   const int k = bk;
@@ -1712,8 +1728,8 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r = lane & 15;
   const int brow = MQ_WAVES * w + q;
-  const int ldN = mix_ldn(N);
-  const int CN = C * ldN;
+  const int ldN = mix_ldn(N);                      // = zR * zL
+  const int CN = C * zL;                           // floats per row segment
   const int nbat = (nv + Bv - 1) / Bv;
   const int total = epochs * nbat;
   const int bc_tail = nv - (nbat - 1) * Bv;
@@ -1732,12 +1748,17 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     bo[i] = n < N ? buf[n] : 0.f;
   }
   int first = *first_flag;
+  // Z layout: zR blocks [n_val][C][zL] (client n = block n / zL, column n % zL; the standard
+  // layout is one block of ldN); a lane's 4-client chunks never straddle a block (zL % 4 == 0)
   uint32_t lofs[NV4];                              // chunks past ldN: out of range (zeros, no access)
 #pragma unroll
-  for (int h = 0; h < NV4; ++h) lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : 0x80000000u;
+  for (int h = 0; h < NV4; ++h) {
+    const int n = n0 + 4 * h;
+    lofs[h] = n < ldN ? 4u * ((uint32_t)(n / zL) * (uint32_t)nv * (uint32_t)CN + (uint32_t)(n % zL)) : 0x80000000u;
+  }
   int sofs[CL];
 #pragma unroll
-  for (int c = 0; c < CL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * ldN);
+  for (int c = 0; c < CL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * zL);
   const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
   int fst = 0, fep = 0, fsb = 0;
   auto fetch_row = [&]() -> int {
@@ -1778,9 +1799,13 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
   int csb = 0;
   int s = 0;
   int late_row = 0;
+#ifdef FS_MIX_STAMPS
+  unsigned long long mr_acc[6] = {0, 0, 0, 0, 0, 0}, mr_prev = 0;
+#endif
 #define QM_STEP(R_)                                                                          \
   {                                                                                          \
     if (s >= total) break;                                                                   \
+    MR_STAMP(0)                                                                              \
     const int bc = min(Bv, nv - csb * Bv);                                                   \
     csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
     float v[16];                                                                             \
@@ -1798,6 +1823,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     _Pragma("unroll") for (int i = 0; i < 4; ++i) v[i] = rs_bank<4>(v[i], v[i + 4]);         \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
     const float opart = rs_pair(v[0], v[1], 1, lane);   /* this workgroup's share */         \
+    MR_STAMP(1)                                                                              \
     const bool real = r < C;                                                                 \
     /* one hop: publish, read the K partials, fold in workgroup order */                     \
     const unsigned tag = (unsigned)s + 1u;                                                   \
@@ -1822,6 +1848,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
       _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
         if (kk < K) o += __uint_as_float((unsigned)gr[kk]);                                  \
     }                                                                                        \
+    MR_STAMP(2)                                                                              \
     /* the late classes of step s - 1 + DEPTH, behind the hop (its polls queue behind nothing) */ \
     if constexpr (SPL < CL) {                                                                \
       if (s > 0) QM_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
@@ -1846,6 +1873,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
       gme[2 * j] = gm2[j].x;                                                                 \
       gme[2 * j + 1] = gm2[j].y;                                                             \
     }                                                                                        \
+    MR_STAMP(3)                                                                              \
     labq[R_] = y[idxq[R_]];                                                                  \
     QM_ISSUE(R_, idxq[R_], 0, SPL);                                                          \
     late_row = idxq[R_];                                                                     \
@@ -1856,7 +1884,9 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = rs_level<16, true>(t[i], t[i + KP], lane); \
     const int par = s & 1;                                                                   \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
+    MR_STAMP(4)                                                                              \
     lds_barrier();                                                                           \
+    MR_STAMP(5)                                                                              \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
       float gs = gx[par][0][lane * KP + i];                                                  \
       _Pragma("unroll") for (int kk = 1; kk < MQ_WAVES; ++kk) gs += gx[par][kk][lane * KP + i]; \
@@ -1865,6 +1895,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     first = 0;                                                                               \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \
     _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
+    MR_STAMP(6)                                                                              \
     ++s;                                                                                     \
     if (pf_prog && k == 0 && (s & 3) == 0) mix_publish_progress(pf_prog, s);                 \
   }
@@ -1886,6 +1917,9 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
       }
     }
     if (k == 0 && lane == 0 && total > 0) *first_flag = 0;
+#ifdef FS_MIX_STAMPS
+    if (k == 0 && lane < 6) reinterpret_cast<unsigned long long*>(buf + N + 8)[lane] = mr_acc[lane];
+#endif
   }
 }
 
@@ -1903,8 +1937,9 @@ static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
 // 1: not covered; 0: launched; < 0: error
 static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
                          int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first, void* d_ws,
-                         int64_t ws_bytes, MixPrefetch pf) {
+                         int64_t ws_bytes, MixPrefetch pf, int zR = 1) {
   if (!qmc_covers(N, C, Bv, nv, epochs)) return 1;
+  const int zL = mix_ldn(N) / zR;
   const int nk = qmc_nk(C);
   const int K = (mix_ldn(N) + 16 * nk - 1) / (16 * nk);
   const int64_t xbytes = mc_xbytes(K);
@@ -1920,13 +1955,13 @@ static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const
   const int zb = (int)((int64_t)nv * C * mix_ldn(N) * 4);
   if (nk == 8)
     hipLaunchKernelGGL((mix_solve_qmc_kernel<8, 10, 2, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
   else if (C <= 10)
     hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 10, 3, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
   else
     hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 16, 2, quad_split<16>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
   return 0;
 }
 
@@ -1948,6 +1983,32 @@ extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   return std::max(mc, (N > 128 && C <= 16 && Bv <= 16) ? qmc : (int64_t)0) + MC_ERR_BYTES;
 }
 
+// L2 prefetch helper setup of fs_mix_solve / fs_mix_solve_blocked (0, or an error status)
+static int mix_prefetch_setup(const fs_tuning& tune, bool use_quad, bool use_qmc, int N, int C, int n_val, void* d_ws,
+                              int64_t ws_bytes, hipStream_t st0, MixPrefetch& pf) {
+  // L2 prefetch helpers (fs_tuning.mix_prefetch: 0 = by solver, -1 = none, n): 4 for the
+  // quarter-wave solver, whose gather they speed up (r02s2k, 1.42-1.47 -> 1.35-1.43 us per step
+  // at config 2), 16 for qmc, none for the others, where they measured nothing; they run
+  // mix_prefetch_lead (0: 16) steps ahead; the progress word lives in the error block (byte 128)
+  // (quad: only when Z outgrows the L2s -- at config 1's 0.6 MB the helpers cost 3 %, r02s2c1)
+  const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
+  const int h = tune.mix_prefetch > 0 ? tune.mix_prefetch
+                : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0)));
+  // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
+  // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
+  // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
+  // 16 is still the fastest: 3.85 us per step vs 4.75 at leads 2-4 (r02s2lead)
+  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : 16;
+  if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
+    pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
+    pf.h = h;
+    pf.lead = lead;
+    hipError_t e = hipMemsetAsync(pf.prog, 0, sizeof(unsigned), st0);
+    if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
+  }
+  return 0;
+}
+
 extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int32_t* d_perms, int N, int C,
                             int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p, float* d_buf,
                             int* d_first, void* d_ws, int64_t ws_bytes, void* stream) {
@@ -1967,28 +2028,7 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   // the multi-CU quarter-wave solver where the single-workgroup register solvers end (N > 256)
   const bool use_qmc = want == FS_SOLVER_QMC || (aut && N > 256 && qmc_covers(N, C, Bv, n_val, epochs));
   MixPrefetch pf{nullptr, 0, 0};
-  {
-    // L2 prefetch helpers (fs_tuning.mix_prefetch: 0 = by solver, -1 = none, n): 4 for the
-    // quarter-wave solver, whose gather they speed up (r02s2k, 1.42-1.47 -> 1.35-1.43 us per step
-    // at config 2), 16 for qmc, none for the others, where they measured nothing; they run
-    // mix_prefetch_lead (0: 16) steps ahead; the progress word lives in the error block (byte 128)
-    // (quad: only when Z outgrows the L2s -- at config 1's 0.6 MB the helpers cost 3 %, r02s2c1)
-    const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
-    const int h = tune.mix_prefetch > 0 ? tune.mix_prefetch
-                  : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0)));
-    // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
-    // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
-    // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
-    // 16 is still the fastest: 3.85 us per step vs 4.75 at leads 2-4 (r02s2lead)
-    const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : 16;
-    if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
-      pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
-      pf.h = h;
-      pf.lead = lead;
-      hipError_t e = hipMemsetAsync(pf.prog, 0, sizeof(unsigned), st0);
-      if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_mix_solve: ") + hipGetErrorString(e));
-    }
-  }
+  if (int rc = mix_prefetch_setup(tune, use_quad, use_qmc, N, C, n_val, d_ws, ws_bytes, st0, pf)) return rc;
   // by shape: one wave for N <= 16, C <= 4; the quarter-wave solver (+ L2 prefetch helpers) for
   // N <= 64, C <= 16 or N <= 128, C <= 10; the register solvers where an instance covers the
   // shape (no cross-CU exchange: ~1-2.5 us per step); for N > 256 the multi-CU quarter-wave
@@ -2083,6 +2123,36 @@ extern "C" int fs_mix_solve(const float* d_Z, const int32_t* d_labels, const int
   hipLaunchKernelGGL(mix_solve_kernel, dim3(1), dim3(MS_THREADS), lds, st, d_Z, d_labels, d_perms, N, C, n_val,
                      epochs, Bv, lr_p, momentum, d_p, d_buf, d_first);
   t_last_solver = 4;
+  FS_LAUNCH_CHECK();
+  return FS_OK;
+}
+
+extern "C" int fs_mix_solve_blocked_covers(int N, int C, int n_val, int epochs, int Bv) {
+  const fs_tuning tune = tuning();
+  const bool forced_other = tune.mix_solver != FS_SOLVER_AUTO && tune.mix_solver != FS_SOLVER_QMC;
+  return !forced_other && N >= 1 && C >= 1 && n_val >= 1 && epochs >= 0 && qmc_covers(N, C, Bv, n_val, epochs) &&
+         (tune.mix_solver == FS_SOLVER_QMC || N > 256);
+}
+
+extern "C" int fs_mix_solve_blocked(const float* d_Z, int blocks, const int32_t* d_labels, const int32_t* d_perms,
+                                    int N, int C, int n_val, int epochs, int Bv, float lr_p, float momentum, float* d_p,
+                                    float* d_buf, int* d_first, void* d_ws, int64_t ws_bytes, void* stream) {
+  FS_REQUIRE(N >= 1 && C >= 1 && n_val >= 1 && epochs >= 0, "bad sizes");
+  FS_REQUIRE(blocks >= 1 && N % (4 * blocks) == 0, "N must be a multiple of 4 * blocks");
+  FS_REQUIRE(Bv >= 1 && Bv <= MS_MAXB, "valid batch size must be in [1, 64]");
+  FS_REQUIRE(d_Z && d_labels && d_perms && d_p && d_buf && d_first, "null pointer");
+  hipStream_t st0 = reinterpret_cast<hipStream_t>(stream);
+  const fs_tuning tune = tuning();
+  if (!fs_mix_solve_blocked_covers(N, C, n_val, epochs, Bv))
+    return fail(FS_EUNSUPPORTED, "fs_mix_solve_blocked: the rank-blocked Z layout is read by the qmc solver only "
+                                 "(N > 256, C <= 16, Bv <= 16); use fs_mix_solve on the standard layout");
+  MixPrefetch pf{nullptr, 0, 0};
+  if (int rc = mix_prefetch_setup(tune, false, true, N, C, n_val, d_ws, ws_bytes, st0, pf)) return rc;
+  const int rc = mix_solve_qmc(st0, d_Z, d_labels, d_perms, N, C, n_val, epochs, Bv, lr_p, momentum, d_p, d_buf,
+                               d_first, d_ws, ws_bytes, pf, blocks);
+  if (rc < 0) return rc;
+  if (rc != 0) return fail(FS_EUNSUPPORTED, "fs_mix_solve_blocked: shape not covered");
+  t_last_solver = FS_SOLVER_QMC;
   FS_LAUNCH_CHECK();
   return FS_OK;
 }

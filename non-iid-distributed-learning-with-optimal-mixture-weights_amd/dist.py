@@ -84,15 +84,19 @@ def solver_layout(shards):
     return L, pos
 
 
-def allgather_z(Z_local, C, out, group=None):
-    """Z_local [n_v, C*L] (this rank's clients, class-major: column c*L + i) -> out
-    [n_v, C*R*L] in solver order (column c*(R*L) + r*L + i), R = world size.  One all-gather
-    of the contiguous per-rank blocks, then one layout copy."""
+def allgather_z(Z_local, C, out, group=None, blocked=False):
+    """Z_local [n_v, C*L] (this rank's clients, class-major: column c*L + i) -> out, R = world
+    size.  ``blocked``: out's storage holds the rank blocks as the all-gather leaves them,
+    [R][n_v][C*L] -- the layout fs_mix_solve_blocked reads (no copy); else out [n_v, C*R*L]
+    in solver order (column c*(R*L) + r*L + i): one all-gather, then one layout copy."""
     nv, CL = Z_local.shape
     L = CL // C
     R = world()[1]
     if R == 1:
         out.copy_(Z_local)
+        return out
+    if blocked:
+        tdist.all_gather_into_tensor(out.view(-1), Z_local.contiguous().view(-1), group=group)
         return out
     buf = torch.empty((R * nv, CL), dtype=Z_local.dtype, device=Z_local.device)    # rank blocks along dim 0
     tdist.all_gather_into_tensor(buf, Z_local.contiguous(), group=group)

@@ -339,6 +339,11 @@ class Mixture:
         self.ws = torch.zeros(int(_lib.lib().fs_mix_solve_ws_bytes(self.N, self.C, self.Bv)), dtype=torch.uint8,
                               device=device)
         self.shuffler = None
+        self.blocks = 1          # > 1: Z holds `blocks` rank blocks [blocks][n_val][C][N/blocks] (dist.py)
+
+    def blocked_covers(self, epochs):
+        """Whether fs_mix_solve_blocked reads this shape (the qmc solver; include/fedsim.h)."""
+        return bool(_lib.lib().fs_mix_solve_blocked_covers(self.N, self.C, self.nv, int(epochs), self.Bv))
 
     def check_errors(self):
         """Raise if a multi-CU p-solve reported a timed-out exchange (synchronises)."""
@@ -374,10 +379,13 @@ class Mixture:
             self.prepare(seeds, slot)
         epochs = self.shuffler.P
         perms = self.shuffler.acquire(slot)
-        _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), _lib.ptr(self.f.labels), _lib.ptr(perms), self.N,
-                                  self.C, self.nv, epochs, self.Bv, float(lr_p), self.momentum,
-                                  _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first),
-                                  _lib.ptr(self.ws), self.ws.numel(), _lib.stream_ptr()), 'fs_mix_solve')
+        tail = (_lib.ptr(self.f.labels), _lib.ptr(perms), self.N, self.C, self.nv, epochs, self.Bv, float(lr_p),
+                self.momentum, _lib.ptr(self.p), _lib.ptr(self.buf), _lib.ptr(self.first), _lib.ptr(self.ws),
+                self.ws.numel(), _lib.stream_ptr())
+        if self.blocks > 1:
+            _lib.check(L.fs_mix_solve_blocked(_lib.ptr(self.Z), self.blocks, *tail), 'fs_mix_solve_blocked')
+        else:
+            _lib.check(L.fs_mix_solve(_lib.ptr(self.Z), *tail), 'fs_mix_solve')
         self.shuffler.release(slot)
         return self.p
 

@@ -185,6 +185,9 @@ class Federation:
                 p0 = torch.zeros(Ns, dtype=torch.float32)
                 p0[torch.from_numpy(self.pos)] = self.p_all
                 self.mixture = engine.Mixture(Xv, yv, D, C, Ns, Bv, p0, dev, ld)
+                # the qmc solver reads the all-gathered rank blocks as they land (no layout copy)
+                if nranks > 1 and self.mixture.blocked_covers(R):
+                    self.mixture.blocks = nranks
                 self.Z_local = torch.empty(self.mixture.nv, C * self.L, device=dev, dtype=torch.float32)
                 lo = self.rank * self.L
                 self.p_slice = lambda p: p[lo:lo + len(mine)]
@@ -290,7 +293,8 @@ class Federation:
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
             self.p_hist[t].copy_(self.mixture.p[self.pos_dev])
             timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local))
-            timed('z_allgather', lambda: dist.allgather_z(self.Z_local, self.C, self.mixture.Z))
+            timed('z_allgather', lambda: dist.allgather_z(self.Z_local, self.C, self.mixture.Z,
+                                                          blocked=self.mixture.blocks > 1))
             if early:
                 torch.cuda.current_stream().wait_stream(self.side)
             p = timed('solve', lambda: self.mixture.solve(None, None, self.lr_p, slot=t % 2, z=False))

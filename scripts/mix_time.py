@@ -1,6 +1,7 @@
 """Diagnostic: fs_mix_solve time per dependent p-SGD step (and fs_mix_z) at a given shape.
-    [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] python scripts/mix_time.py [N] [C] [n_val] [epochs]
-(GPU box; default config 2; the two variables only select fs_tuning fields for this run)"""
+    [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] [FS_MIX_PF_H=h] [FS_MIX_PF_LEAD=l] python scripts/mix_time.py
+        [N] [C] [n_val] [epochs] [D]
+(GPU box; default config 2; the variables only select fs_tuning fields for this run)"""
 import os
 import sys
 
@@ -12,10 +13,11 @@ import fedamw_amd  # noqa: E402,F401
 from fedamw_amd import engine, rng  # noqa: E402
 
 SOLVER = os.environ.get('FS_MIX_SOLVER', 'auto')
-fedamw_amd._lib.set_tuning(mix_solver=SOLVER, mix_exact_softmax=int(os.environ.get('FS_MIX_EXACT', '0')))
+fedamw_amd._lib.set_tuning(mix_solver=SOLVER, mix_exact_softmax=int(os.environ.get('FS_MIX_EXACT', '0')),
+                           mix_prefetch=int(os.environ.get('FS_MIX_PF_H', '0')),
+                           mix_prefetch_lead=int(os.environ.get('FS_MIX_PF_LEAD', '0')))
 a = [int(x) for x in sys.argv[1:]]
-N, C, nv, ep = (a + [100, 10, 12800, 10][len(a):])[:4]
-D = 2048
+N, C, nv, ep, D = (a + [100, 10, 12800, 10, 2048][len(a):])[:5]
 dev = torch.device('cuda')
 g = torch.Generator().manual_seed(0)
 Xv = torch.cos(torch.randn(nv, D, generator=g)) / D ** 0.5
@@ -55,8 +57,10 @@ print('  solver requested %s, ran %s' % (SOLVER,
                                          L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]), flush=True)
 if STAMPS:
     acc = mix.buf[N + 8:N + 20].cpu().numpy().view(np.uint64)
-    names = (['wait+logits', 'rs+softmax+grad', 'fold', 'barrier', 'update+gather', 'issue']
-             if SOLVER == 'quad' else
-             ['wait ring', 'logits+softmax+grad', 'gpart+issue', 'barrier', 'update'])
+    ran = L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]
+    names = {'quad': ['wait+logits', 'rs+softmax+grad', 'fold', 'barrier', 'update+gather', 'issue'],
+             'qmc': ['wait ring+logits+rs', 'hop (publish+polls)', 'late issue+softmax+grad', 'issue+fold+lds',
+                     'barrier', 'update+gather']}.get(ran, ['wait ring', 'logits+softmax+grad', 'gpart+issue',
+                                                           'barrier', 'update'])
     print('wave-0 s_memtime ticks per step (last call): ' +
           ', '.join('%s %.0f' % (nm, a / steps) for nm, a in zip(names, acc)), flush=True)

@@ -7,8 +7,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import fedamw_amd  # noqa: E402,F401
-
-L = fedamw_amd._lib
+from fedamw_amd import _lib as L  # noqa: E402
 a = [int(x) for x in sys.argv[1:]]
 N, C, D, nv, reps = (a + [1000, 10, 16384, 32000, 5][len(a):])[:5]
 dev = torch.device('cuda')

@@ -60,6 +60,68 @@ def _worker(rank, world, port, algo, out):
         torch.distributed.destroy_process_group()
 
 
+def _problem_wide():
+    """300 clients: the sharded p-solve (solver N = 2 x 152) runs qmc on the all-gathered rank
+    blocks in place (fs_mix_solve_blocked), the single-process one qmc on [n_v][C][300]."""
+    rs = np.random.RandomState(5)
+    D, C = 64, 6
+    sizes = list(rs.randint(3, 14, size=300))
+    Xs = [(np.cos(rs.normal(size=(n, D))) / np.sqrt(D)).astype(np.float32) for n in sizes]
+    ys = [rs.randint(0, C, size=n).astype(np.int64) for n in sizes]
+    Xt = (np.cos(rs.normal(size=(70, D))) / np.sqrt(D)).astype(np.float32)
+    yt = rs.randint(0, C, size=70).astype(np.int64)
+    Xv = (np.cos(rs.normal(size=(150, D))) / np.sqrt(D)).astype(np.float32)
+    yv = rs.randint(0, C, size=150).astype(np.int64)
+    return D, C, Xs, ys, Xt, yt, Xv, yv
+
+
+def _run_wide():
+    import fedamw_amd
+    from fedamw_amd import _lib
+    from fedamw_amd.functions import tools
+    D, C, Xs, ys, Xt, yt, Xv, yv = _problem_wide()
+    T = torch.from_numpy
+    torch.manual_seed(12)
+    vl = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(T(Xv), T(yv)), batch_size=16, shuffle=True)
+    fed = tools.Federation('fedamw', [T(x) for x in Xs], [T(y) for y in ys], T(Xt), T(yt), vl, 'classification', C,
+                           D, 0.5, 2, 32, False, 0.0, True, 1e-3, 2, 0.01, 'parallel', verbose=False)
+    for _ in range(2):
+        fed.round()
+    out = fed.results()
+    solver = _lib.SOLVER_NAMES[_lib.lib().fs_mix_solve_last_mode()]
+    p = fed.mixture.p[fed.pos_dev].cpu().numpy() if fed.zshard else fed.mixture.p.cpu().numpy()
+    return [o.numpy() for o in out], fed.W_g[:, :D].cpu().numpy(), p, solver, fed.mixture.blocks
+
+
+def _worker_wide(rank, world, port, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        out[rank] = _run_wide()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_sharded_fedamw_reads_rank_blocks():
+    """SURVEY 8(e) sharded FedAMW at 300 clients on 2 ranks: the all-gathered Z stays in its
+    rank blocks and the qmc solver reads them in place (no layout copy); the result matches the
+    single-process run (qmc on the standard layout, a different client-to-workgroup split of
+    the same sums) within the fp32 tolerances."""
+    ref, Wref, pref, solver, blocks = _run_wide()
+    assert solver == 'qmc' and blocks == 1
+    mgr = mp.get_context('spawn').Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_wide, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        res, W, p, solver, blocks = out[r]
+        assert solver == 'qmc' and blocks == 2
+        assert np.abs(p - pref).max() <= 1e-5 * np.abs(pref).max()
+        assert np.abs(W - Wref).max() <= 1e-5 * np.abs(Wref).max()
+        np.testing.assert_allclose(res[0], ref[0], atol=1e-5)
+        np.testing.assert_allclose(res[1], ref[1], atol=1e-5)
+    assert np.array_equal(out[0][2], out[1][2])            # the replicated solve: identical p
+
+
 @pytest.mark.parametrize('algo', ['fedavg', 'fedprox', 'fedamw'])
 def test_sharded_matches_single_process(algo):
     ref, Wref = _run(algo)

@@ -9,7 +9,8 @@ import torch
 
 from oracle import fedsim_oracle as O
 from tests.fixtures import (BENCH_CASES, HORIZON_CASES, LONG_CASES, LOSS_RTOL, P_RTOL, ROUND_CASES, TRAIN_UNITS,
-                            W_RTOL, acc_tol, horizon_rtol, load, load_bench, load_horizon, load_long, positional, split_clients)
+                            W_RTOL, acc_tol, horizon_rtol, load, load_bench, load_horizon, load_long, positional,
+                            split_clients)
 
 pytestmark = pytest.mark.gpu
 
@@ -110,9 +111,10 @@ def test_dropin_benchmark_length_fedamw(amd, name):
 def test_dropin_solver_horizon_fedamw(amd, name):
     """The FedAMW drop-in against the reference at the horizons of the two p-solvers configs 1
     and 5 run (tools.py:423 -- momentum persisting across rounds -- and 441-453): ``qmc``, the
-    multi-CU solver of config 5 (N = 300 > 256, C = 10, R = 20 rounds of >= 1,200 dependent
-    momentum steps, lr_p = 1e-3 as in the configs) and ``bin``, config 1's two-class solver
-    (N = 10, C = 2, n_v = 6,509: 4,070 steps per round, R = 10); chained and parallel clients.
+    multi-CU solver of config 5 (N = 300 > 256, C = 10, R = 20 rounds of 1,740 dependent
+    momentum steps; lr_p = 3e-4, at the configs' 1e-3 the reference itself diverges here, see
+    make_golden.py HORIZON) and ``bin``, config 1's two-class solver (N = 10, C = 2, n_v = 6,509:
+    4,070 steps per round, R = 10, lr_p = 1e-3); chained and parallel clients.
     Every round's global model and mixture weights, the losses, the accuracy and where the
     generator is left."""
     d = load_horizon(name)
@@ -688,6 +690,46 @@ def test_mix_z_shapes(amd, N, C, D, nv):
     assert (np.abs(Z[:, :, :N] - ref) <= 2e-6 * scale + 1e-30).all()
     assert (Z[:, :, N:] == 0).all()
     assert (Zb[nv] == 7.0).all()
+
+
+@pytest.mark.parametrize('N,blocks,C', [(304, 2, 10), (384, 4, 10), (1024, 8, 10), (520, 2, 13)])
+def test_mix_solve_blocked_layout_bitwise(amd, N, blocks, C):
+    """fs_mix_solve_blocked on the rank-blocked Z an all-gather leaves ([blocks][n_val][C][L],
+    dist.allgather_z(blocked=True)) == fs_mix_solve on the same Z in solver order, BITWISE in p
+    and the momentum buffer (same solver, same arithmetic, only the addresses differ), over two
+    calls; shapes the blocked form does not read are refused with FS_EUNSUPPORTED."""
+    rs = np.random.RandomState(N + blocks)
+    D, nv, ep = 64, 333, 3
+    L = N // blocks
+    dev = torch.device('cuda')
+    Xv = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
+    yv = torch.from_numpy(rs.randint(0, C, size=nv).astype(np.int64))
+    p0 = torch.from_numpy(rs.dirichlet(np.ones(N)).astype(np.float32))
+    W = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.5).astype(np.float32)).to(dev)
+    std = amd.engine.Mixture(Xv, yv, D, C, N, 16, p0, dev)
+    blk = amd.engine.Mixture(Xv, yv, D, C, N, 16, p0, dev)
+    assert blk.blocked_covers(ep)
+    blk.blocks = blocks
+    Wd = torch.zeros(N, C, std.f.ld, device=dev)
+    Wd[:, :, :D] = W
+    L_ = amd.lib
+    L_.check(L_.lib().fs_mix_z(L_.ptr(Wd), L_.ptr(std.f.phi), std.f.ld, N, C, nv, L_.ptr(std.Z), L_.stream_ptr()), 'z')
+    # the blocked image: rank block r holds columns r*L .. r*L+L-1 of every class
+    blk.Z.view(-1).copy_(std.Z.view(nv, C, blocks, L).permute(2, 0, 1, 3).reshape(-1))
+    for call in range(2):
+        torch.manual_seed(70 + call)
+        seeds = amd.rng.draw_pass_seeds(ep)
+        std.solve(None, seeds, 0.01, z=False)
+        blk.solve(None, seeds, 0.01, z=False)
+        torch.cuda.synchronize()
+        assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
+        assert torch.equal(std.p, blk.p) and torch.equal(std.buf, blk.buf), call
+    assert bool(torch.isfinite(std.p).all()) and not torch.equal(std.p, p0.to(dev))
+    small = amd.engine.Mixture(Xv, yv, D, C, 200, 16, torch.full((200,), 0.005), dev)
+    assert not small.blocked_covers(ep)                 # N <= 256: not the qmc solver's shape
+    small.blocks = 2
+    with pytest.raises(amd.lib.FedsimError, match='qmc solver only'):
+        small.solve(None, amd.rng.draw_pass_seeds(1), 0.01, z=False)
 
 
 def test_mix_z_and_solve_vs_oracle(amd):
