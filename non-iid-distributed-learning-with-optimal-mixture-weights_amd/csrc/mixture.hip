@@ -1897,7 +1897,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
     MR_STAMP(6)                                                                              \
     ++s;                                                                                     \
-    if (pf_prog && k == 0 && (s & 3) == 0) mix_publish_progress(pf_prog, s);                 \
+    if (pf_prog && k == 0) mix_publish_progress(pf_prog, s);   /* every step: helpers pace on it */ \
   }
   for (;;) {
     QM_STEP(0)
