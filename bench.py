@@ -99,8 +99,6 @@ def parse(argv=None):
                     help="fs_tuning.train_form: the local-training kernel form for parallel clients (A/B runs)")
     ap.add_argument('--launch-timeout', type=float, default=1800.0,
                     help='--gpus N launcher: wall-clock bound on the workers (seconds; 0 = none)')
-    ap.add_argument('--stream-form', choices=['auto', 'on', 'off'], default='auto',
-                    help="fs_tuning.stream_form: the 4-wave double-buffered split form (A/B runs)")
     ap.add_argument('--split-early', choices=['auto', 'off'], default='auto',
                     help="fs_tuning.split_early: the split form's early row issue (A/B runs)")
     a = ap.parse_args(argv)
@@ -470,7 +468,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                      'traffic': (rec or {}).get('bytes_per_launch'), 'traffic_note': tnote,
                      'mfma_busy': (rec or {}).get('mfma_busy'),
                      'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes, 'group_width': fed.trainer.width,
-                     'form': _form(fed)},
+                     'form': 'pair' if fed.trainer.pair else ('split' if fed.trainer.G > 1 else 'single')},
         'final_test_acc': float(ta[fed.t - 1]),
     }
     if fedamw:
@@ -505,16 +503,6 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
     return out
 
 
-def _form(fed):
-    """The local-training kernel form the launch ran (fs_local_train_plan + fs_tuning)."""
-    from fedamw_amd import _lib
-    if fed.trainer.pair:
-        return 'pair'
-    if fed.trainer.G <= 1:
-        return 'single'
-    return 'stream' if _lib.lib().fs_local_train_last_form() == 2 else 'split'
-
-
 def _solver_name():
     from fedamw_amd import _lib
     return _lib.SOLVER_NAMES.get(_lib.lib().fs_mix_solve_last_mode(), '?')
@@ -532,8 +520,7 @@ def worker(args):
     ws, rank, dev, dinfo = setup_rank(args)
     from fedamw_amd import _lib as flib
     flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2}[args.train_form],
-                    split_early={'auto': 0, 'off': -1}[args.split_early],
-                    stream_form={'auto': 0, 'on': 1, 'off': -1}[args.stream_form])
+                    split_early={'auto': 0, 'off': -1}[args.split_early])
     wl = {k: getattr(args, k) for k in ('algo', 'clients', 'rows', 'D', 'C', 'test', 'shape')}
     wl['config'] = args.config
     headline = (args.config == 2 and not args.custom)

@@ -76,10 +76,6 @@ const char* fs_last_error(void);
  *   train_form         (ABI 10) fs_local_train_plan's choice for parallel clients: 0 = by shape
  *                      (the pair form where it fits, else the split form), 1 = never the pair
  *                      form, 2 = the pair form wherever it fits (else as 0)
- *   stream_form        (ABI 12) split clients without a prox anchor on full slices of 16
- *                      tiles (ld = 1024 G, 16 < B <= 32): 1 = the 4-wave, double-buffered
- *                      stream form (local_train_stream.hip; bitwise the split form), -1 =
- *                      never, 0 = by shape
  *   split_early        (ABI 11) split form without a prox anchor on full slices: 0 = issue the
  *                      first SP_E1 (local_train_split.hip: 4 at G = 2, 6 at G >= 4) of each
  *                      wave's 16 next-step row loads right after the hand-off (they stream
@@ -106,7 +102,6 @@ typedef struct fs_tuning {
   int inject_timeout;
   int train_form;
   int split_early;
-  int stream_form;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -195,9 +190,6 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
 #define FS_G_PAIR 256
 int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                         int* G_out, int64_t* ws_bytes_out);
-/* (ABI 12) the form the calling thread's last split launch ran: 1 = the split form, 2 = the
- * stream form (fs_tuning.stream_form), 0 = none yet (diagnostics; the pair form is G | FS_G_PAIR) */
-int fs_local_train_last_form(void);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                    const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
                    float lr, float mu, int prox, float lam, int reg, int chained,

@@ -19,7 +19,6 @@ _SIGS = {
     'fs_tuning_size': (C.c_int64, []),
     'fs_set_tuning': (C.c_int, [C.c_void_p]),
     'fs_set_thread_tuning': (C.c_int, [C.c_void_p]),
-    'fs_local_train_last_form': (C.c_int, []),
     'fs_get_tuning': (C.c_int, [C.c_void_p]),
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     'fs_libsvm_scan': (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -82,7 +81,7 @@ class Tuning(C.Structure):
     _fields_ = [('mix_solver', C.c_int), ('mix_prefetch', C.c_int), ('mix_prefetch_lead', C.c_int),
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
-                ('split_early', C.c_int), ('stream_form', C.c_int)]
+                ('split_early', C.c_int)]
 
 
 class PlanDesc(C.Structure):
@@ -208,8 +207,8 @@ def stream_ptr(stream=None):
 
 # the device sources each measured kernel is compiled from (its own file + the headers it includes)
 KERNEL_SOURCES = {
-    'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_stream.hip', 'local_train_pair.hip',
-                    'split_common.h', 'common.h', 'eval_rows.h', 'lanes.h'),
+    'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_pair.hip', 'split_common.h', 'common.h',
+                    'eval_rows.h', 'lanes.h'),
     'mix_solve': ('mixture.hip', 'common.h', 'lanes.h'),
     'mix_z': ('mix_z.hip', 'common.h'),
 }

@@ -10,13 +10,17 @@
 
 namespace fs {
 
-// wave w's partial logits of the 16-row group (tiles w, w + NWV, w + 2 NWV, ...) into zt
-template <int NWV, int CT>
-__device__ __forceinline__ void eval_wave16(const float* xr, bool rok, int64_t ld, int NT, const float* __restrict__ W,
-                                            int C, int w, int lane, float* zt) {
-  const int l16 = lane & 15, lg = lane >> 4;
+// zt: NWV * 16 * (16 CT + 1) floats of LDS.  ce / cor accumulate in wave 0's lanes 0-15.
+template <int NWV, int CT = 1>
+__device__ __forceinline__ void eval_group16(const float* __restrict__ phi, int64_t ld, const int32_t* __restrict__ y,
+                                             int n, const float* __restrict__ W, int C, int r0, float* zt, double& ce,
+                                             double& cor) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int NT = (int)(ld >> 6);
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int ZS = CT * 16 + 1;
+  const bool rok = r0 + l16 < n;
+  const float* xr = phi + (int64_t)(rok ? r0 + l16 : 0) * ld;
+  constexpr int ZS = CT * 16 + 1;                  // LDS row stride of the partial logits
   floatx4 acc[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -53,27 +57,8 @@ __device__ __forceinline__ void eval_wave16(const float* xr, bool rok, int64_t l
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
     for (int i = 0; i < 4; ++i) zt[(w * 16 + 4 * lg + i) * ZS + ct * 16 + l16] = acc[ct][i];
-}
-
-// zt: NWV * 16 * (16 CT + 1) floats of LDS.  ce / cor accumulate in wave 0's lanes 0-15.
-// VPR > 1: NWV / VPR real waves each run VPR of the NWV (virtual) waves' partials, kept apart
-// -- the same bits as NWV real waves (the 4-wave stream form's fused evaluation).
-template <int NWV, int CT = 1, int VPR = 1>
-__device__ __forceinline__ void eval_group16(const float* __restrict__ phi, int64_t ld, const int32_t* __restrict__ y,
-                                             int n, const float* __restrict__ W, int C, int r0, float* zt, double& ce,
-                                             double& cor) {
-  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15;
-  const int NT = (int)(ld >> 6);
-  const bool rok = r0 + l16 < n;
-  const float* xr = phi + (int64_t)(rok ? r0 + l16 : 0) * ld;
-  constexpr int ZS = CT * 16 + 1;                  // LDS row stride of the partial logits
-#pragma unroll
-  for (int u = 0; u < VPR; ++u) {
-    const int w = (tid >> 6) + (NWV / VPR) * u;    // the (virtual) wave
-    eval_wave16<NWV, CT>(xr, rok, ld, NT, W, C, w, lane, zt);
-  }
   __syncthreads();
-  if ((tid >> 6) == 0 && lane < 16 && r0 + lane < n) {
+  if (w == 0 && lane < 16 && r0 + lane < n) {
     const int r = lane;
     const int yy = y[r0 + r];
     float m = -INFINITY;
@@ -94,12 +79,12 @@ __device__ __forceinline__ void eval_group16(const float* __restrict__ phi, int6
 }
 
 // block e of E walks the row groups e, e + E, ... and writes its two partial sums to part[2e]
-template <int NWV, int VPR = 1>
+template <int NWV>
 __device__ void eval_persistent(const float* __restrict__ phi, int64_t ld, const int32_t* __restrict__ y, int n,
                                 const float* __restrict__ W, int C, int e, int E, float* zt,
                                 double* __restrict__ part) {
   double ce = 0.0, cor = 0.0;
-  for (int rg = e; rg * 16 < n; rg += E) eval_group16<NWV, 1, VPR>(phi, ld, y, n, W, C, rg * 16, zt, ce, cor);
+  for (int rg = e; rg * 16 < n; rg += E) eval_group16<NWV>(phi, ld, y, n, W, C, rg * 16, zt, ce, cor);
   if ((threadIdx.x >> 6) == 0) {
     ce = wave_sum(ce);
     cor = wave_sum(cor);

@@ -49,8 +49,6 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": train_form must be 0, 1 or 2");
   if (t && (t->split_early < -1 || t->split_early > 0))
     return fail(FS_EINVAL, std::string(fn) + ": split_early must be -1 or 0");
-  if (t && (t->stream_form < -1 || t->stream_form > 1))
-    return fail(FS_EINVAL, std::string(fn) + ": stream_form must be -1, 0 or 1");
   return FS_OK;
 }
 

@@ -689,25 +689,8 @@ static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t
   hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
 }
 
-bool stream_fits(const LTParams& P, int G);
-int launch_local_train_stream(const LTParams& P, int G, const SplitWS& X, int grid, size_t lds, hipStream_t st);
-
-// fs_tuning.stream_form: 0 = by shape, 1 = the 4-wave stream form wherever it fits, -1 = never
-static bool use_stream(const LTParams& P, int RT, int G) {
-  const int f = tuning().stream_form;
-  return RT == 2 && f > 0 && stream_fits(P, G);
-}
-
-static thread_local int t_last_form = 0;    // fs_local_train_last_form
-
 template <int RT, int G>
 static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (use_stream(P, RT, G)) {
-    (void)launch_local_train_stream(P, G, X, grid, lds, st);
-    t_last_form = 2;
-    return;
-  }
-  t_last_form = 1;
   // early row issue where every workgroup's slice is full (NT = G * 16 tiles) and no prox
   // anchor is re-read (fs_tuning.split_early: 0 = by shape, -1 = never)
   // Depth per width (profiles/r03/split_early_ab2.txt, launch ms): at G = 2 (128 KB of rows per
@@ -855,5 +838,3 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   *ws_bytes_out = split_ws_bytes(N, G, B, chained, cus);
   return FS_OK;
 }
-
-extern "C" int fs_local_train_last_form(void) { return fs::t_last_form; }

@@ -20,8 +20,6 @@ from scripts.lt_sweep import SHAPES  # noqa: E402
 NAMES = ['fwd', 'S1', 'sum+publish', 'poll+sum', 'next(early)', 'S2', 'softmax+S3+next', 'bwd+update']
 PAIR_NAMES = ['wait rows', 'fwd', 'S1', 'publish+img', 'wait polls', 'check', 'sum+S2', 'softmax+S3',
               'issue', 'bwd+update']
-STREAM_NAMES = ['fwd(+LF loads)', 'S1', 'sum+publish', 'polls+LH loads+img+check', 'S2', 'softmax+S3',
-                'bwd+update(+rest)']
 
 
 def main():
@@ -30,10 +28,7 @@ def main():
     ap.add_argument('--G', type=int, default=0)
     ap.add_argument('--chained', action='store_true')
     ap.add_argument('--pair', action='store_true', help='the pair form at width --G (or the planner\'s)')
-    ap.add_argument('--stream', action='store_true', help='the 4-wave stream form (fs_tuning.stream_form = 1)')
     a = ap.parse_args()
-    if a.stream:
-        fedamw_amd._lib.set_tuning(stream_form=1)
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
@@ -55,8 +50,6 @@ def main():
     for _ in range(3):
         tr.run(W0, 0.5, False, 0, True, 1e-5, chained)
     torch.cuda.synchronize()
-    if not tr.pair and fedamw_amd._lib.lib().fs_local_train_last_form() == 2:
-        names = STREAM_NAMES
     tr.check_errors()
     st = tr.ws[base:base + extra].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
     st = st[st[:, 15] > 0]
