@@ -1838,12 +1838,22 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
       _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
         if (kk < K) gr[kk] = __hip_atomic_load(slot + (int64_t)kk * MC_SLOT + gi, __ATOMIC_RELAXED, \
                                                __HIP_MEMORY_SCOPE_AGENT);                    \
-      _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk) {                              \
-        if (kk < K && !dead && (unsigned)(gr[kk] >> 32) != tag) {                            \
-          unsigned long long g_ = 0;                                                         \
-          if (mc_wait(slot + (int64_t)kk * MC_SLOT + gi, tag, g_, spin_limit, err)) gr[kk] = g_; \
-          else dead = true;                                                                  \
+      /* re-poll every partner still missing in ONE batch per round trip (round 3 spun on   \
+         them one after another: a round trip per late partner) */                           \
+      for (unsigned spins = 0; !dead;) {                                                     \
+        bool miss = false;                                                                   \
+        _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                              \
+          miss |= kk < K && (unsigned)(gr[kk] >> 32) != tag;                                 \
+        if (!miss) break;                                                                    \
+        if (++spins > spin_limit) {                                                          \
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);           \
+          dead = true;                                                                       \
+          break;                                                                             \
         }                                                                                    \
+        _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                              \
+          if (kk < K && (unsigned)(gr[kk] >> 32) != tag)                                     \
+            gr[kk] = __hip_atomic_load(slot + (int64_t)kk * MC_SLOT + gi, __ATOMIC_RELAXED,  \
+                                       __HIP_MEMORY_SCOPE_AGENT);                            \
       }                                                                                      \
       _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
         if (kk < K) o += __uint_as_float((unsigned)gr[kk]);                                  \
@@ -1993,12 +2003,12 @@ static int mix_prefetch_setup(const fs_tuning& tune, bool use_quad, bool use_qmc
   // (quad: only when Z outgrows the L2s -- at config 1's 0.6 MB the helpers cost 3 %, r02s2c1)
   const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
   const int h = tune.mix_prefetch > 0 ? tune.mix_prefetch
-                : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 16 : 0)));
-  // default lead 16 steps.  At config 5 (640 KB of Z rows per step) the prefetched lines do
-  // not survive in the 4 MB L2 -- the launch fetches twice its algorithmic bytes from HBM
-  // (profiles/r02/pmc_c5_fedamw.txt) -- but they land in the Infinity Cache, and a lead of
-  // 16 is still the fastest: 3.85 us per step vs 4.75 at leads 2-4 (r02s2lead)
-  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : 16;
+                : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 24 : 0)));
+  // default lead: 16 steps for the quarter-wave solver; 6 for qmc, whose helpers (round 4:
+  // LDS-DMA pieces, the solver's progress published every step) keep 6 x 640 KB of rows in
+  // the XCD's 4 MB L2 ahead of the solver at config 5 -- 24 helpers, leads 4 / 6 / 8 / 12:
+  // 3.85 / 3.62 / 3.76 / 3.81 us per step, none: 4.40 (profiles/r04/mix_solve_helper_sweep.txt)
+  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : (use_qmc ? 6 : 16);
   if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
     pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
     pf.h = h;

@@ -13,7 +13,7 @@ run() {   # H LEAD N C NV EP
     || { echo "mix_time rc=$? (H=$1 lead=$2 N=$3)"; tail -20 $OUT; exit 1; }
   echo "  ^ H=$1 lead=$2" >> $OUT
 }
-PAIRS=${*:-"0:0 -1:0 24:4 24:6 24:8 24:12 16:6"}
+PAIRS=${*:-"0:0 -1:0 24:8 16:6"}
 for hl in $PAIRS; do run ${hl%%:*} ${hl##*:} 1000 10 32000 5; done
-for hl in 0:0 -1:0 4:4; do run ${hl%%:*} ${hl##*:} 100 10 12800 10; done
+for hl in 0:0; do run ${hl%%:*} ${hl##*:} 100 10 12800 10; done
 cat $OUT
