@@ -324,7 +324,7 @@ def cpu_baseline(d, wl, budget, fedamw, rounds_R, z_rows=None):
     threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
     whole = bool(rounds) and not fedamw
     return {'value': N / t_round, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
-            'measured': whole, 'extrapolation_factor': t_round / el,
+            'measured': whole, 'extrapolation_factor': 1.0 if whole else t_round / el,
             'sample': sample + ' of the numpy oracle, %.1f s, %s' % (
                 el, 'whole rounds' if whole else 'extrapolated to whole rounds (x%.0f)' % (t_round / el))}
 

@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 12
+#define FS_ABI_VERSION 13
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -62,9 +62,9 @@ const char* fs_last_error(void);
  *   mix_solver         0 = by shape, else force one p-solver (FS_SOLVER_*; a forced solver
  *                      that does not cover the shape falls through to the shape's choice)
  *   mix_prefetch       L2 prefetch helper workgroups beside the p-solve: 0 = by solver
- *                      (4 for the quarter-wave solver when Z outgrows the L2s, 16 for qmc),
+ *                      (4 for the quarter-wave solver when Z outgrows the L2s, 24 for qmc),
  *                      -1 = none, n > 0 = n
- *   mix_prefetch_lead  steps the helpers run ahead (0 = 16)
+ *   mix_prefetch_lead  steps the helpers run ahead (0 = by solver: 16 quad, 6 qmc)
  *   mix_exact_softmax  quarter-wave solvers: 1 = torch's exp(o - m - log sum) form with libm
  *                      expf / logf (default: e * rcp(sum e) on v_exp_f32 / v_rcp_f32; both
  *                      within the fp32 tolerance of the reference)
@@ -80,6 +80,10 @@ const char* fs_last_error(void);
  *                      first SP_E1 (local_train_split.hip: 4 at G = 2, 6 at G >= 4) of each
  *                      wave's 16 next-step row loads right after the hand-off (they stream
  *                      through the softmax), -1 = all of them inside the backward
+ *   mix_qmc_lane_clients (ABI 13) qmc p-solver: clients per lane, 0 = by shape (8 for
+ *                      C <= 10, else 4), 4 = force 4 (K = ceil(N / 64) workgroups, <= 16),
+ *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
+ *                      of the K-partial sums (a different client-to-workgroup split)
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -102,6 +106,7 @@ typedef struct fs_tuning {
   int inject_timeout;
   int train_form;
   int split_early;
+  int mix_qmc_lane_clients;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);

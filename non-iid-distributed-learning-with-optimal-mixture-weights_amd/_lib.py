@@ -67,7 +67,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
@@ -81,7 +81,7 @@ class Tuning(C.Structure):
     _fields_ = [('mix_solver', C.c_int), ('mix_prefetch', C.c_int), ('mix_prefetch_lead', C.c_int),
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
-                ('split_early', C.c_int)]
+                ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int)]
 
 
 class PlanDesc(C.Structure):
@@ -111,7 +111,7 @@ def lib():
     FEDSIM_LIB overrides the path (diagnostic builds, e.g. the in-kernel stamp build)."""
     global _lib
     if _lib is None:
-        path = os.environ.get('FEDSIM_LIB', LIB_PATH)
+        path = os.environ.get('FEDSIM_LIB') or LIB_PATH
         if not os.path.exists(path):
             raise FedsimError(
                 'libfedsim.so not found at %s -- build it with `python -c "import __graft_entry__ as g; g.build()"` '

@@ -49,6 +49,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": train_form must be 0, 1 or 2");
   if (t && (t->split_early < -1 || t->split_early > 0))
     return fail(FS_EINVAL, std::string(fn) + ": split_early must be -1 or 0");
+  if (t && t->mix_qmc_lane_clients != 0 && t->mix_qmc_lane_clients != 4 && t->mix_qmc_lane_clients != 8)
+    return fail(FS_EINVAL, std::string(fn) + ": mix_qmc_lane_clients must be 0, 4 or 8");
   return FS_OK;
 }
 

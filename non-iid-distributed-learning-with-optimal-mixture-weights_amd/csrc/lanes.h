@@ -135,6 +135,29 @@ __device__ __forceinline__ float row16_all(float x) {
   return x;
 }
 
+// x of lane c of this lane's 16-lane row (gfx950 DPP row_newbcast:c; c a compile-time
+// constant after unrolling)
+__device__ __forceinline__ float row_get(float x, int c) {
+  switch (c) {
+    case 0: return dpp<0x150>(x);
+    case 1: return dpp<0x151>(x);
+    case 2: return dpp<0x152>(x);
+    case 3: return dpp<0x153>(x);
+    case 4: return dpp<0x154>(x);
+    case 5: return dpp<0x155>(x);
+    case 6: return dpp<0x156>(x);
+    case 7: return dpp<0x157>(x);
+    case 8: return dpp<0x158>(x);
+    case 9: return dpp<0x159>(x);
+    case 10: return dpp<0x15A>(x);
+    case 11: return dpp<0x15B>(x);
+    case 12: return dpp<0x15C>(x);
+    case 13: return dpp<0x15D>(x);
+    case 14: return dpp<0x15E>(x);
+    default: return dpp<0x15F>(x);
+  }
+}
+
 // the two values of a permlane swap of x with itself: lo = x of the lane group with the
 // OFF bit clear, hi = x of the group with it set (OFF = 16: rows; 32: halves)
 template <int OFF>

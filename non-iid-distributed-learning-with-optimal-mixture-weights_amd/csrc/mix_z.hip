@@ -11,7 +11,8 @@
 // Design (round 4; replaces the 64x64 / BK 16 / two-barrier tile GEMM that ran 105 TFLOP/s
 // with 50 % LDS bank-conflict cycles):
 //  * 256-thread workgroup (one wave per SIMD), 256 x 128 output tile, each wave 128 x 64 =
-//    4 x 2 blocks of 32 x 32 (128 accumulator registers);
+//    4 x 2 blocks of 32 x 32 (128 accumulator registers); 128 x 128 tiles (wave 64 x 64) when
+//    256-row tiles would not give every CU one;
 //  * K-step 32 (one 128-B line per row): A image 256 rows x 128 B, B image 128 rows x 128 B,
 //    filled by global_load_lds_dwordx4 (LDS-DMA, no VGPR staging) in pieces of 8 rows x
 //    128 B -- 48 pieces per K-step, 12 per wave -- into two LDS buffers (2 x 48 KB): the next
@@ -35,13 +36,17 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __host__ __device__ __forceinline__ int mixz_ldn(int N) { return (N + 3) & ~3; }
 
-constexpr int ZG_BM = 256, ZG_BN = 128, ZG_BK = 32;
+// BM = 256 (each wave 128 x 64: MB = 4 row blocks of 32) where the grid gives every CU a tile
+// (config 2: 400 tiles on 256 CUs); BM = 128 (MB = 2) for smaller grids
+constexpr int ZG_BN = 128, ZG_BK = 32;
 constexpr int ZG_ROWB = ZG_BK * 4;                       // 128 B per row per K-step
-constexpr int ZG_ABYTES = ZG_BM * ZG_ROWB;               // 32 KB
-constexpr int ZG_BUFB = (ZG_BM + ZG_BN) * ZG_ROWB;       // 48 KB per buffer
-constexpr int ZG_PIECES = (ZG_BM + ZG_BN) / 8;           // 48 pieces of 8 rows x 128 B
-constexpr int ZG_PPW = ZG_PIECES / 4;                    // 12 per wave
 constexpr int ZG_GROUP_M = 8;                            // row tiles per tile-order group
+template <int BM> struct ZgShape {
+  static constexpr int MB = BM / 64;                     // 32-row blocks per wave
+  static constexpr int ABYTES = BM * ZG_ROWB;            // 32 / 16 KB
+  static constexpr int BUFB = (BM + ZG_BN) * ZG_ROWB;    // 48 / 32 KB per buffer
+  static constexpr int PPW = (BM + ZG_BN) / 8 / 4;       // pieces of 8 rows x 128 B per wave: 12 / 8
+};
 
 __device__ __forceinline__ void zg_glds(const float* g, char* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -54,19 +59,21 @@ __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
 
 // one K-step from one buffer: per kq, 4 + 2 ds_read_b128 feed 4 x 8 MFMAs; the fragments of
 // kq + 1 are read while the MFMAs of kq run (two register sets)
-__device__ __forceinline__ void zg_frags(const char* cur, int a_off, int b_off, int frag, float4 (&a)[4],
+template <int MB>
+__device__ __forceinline__ void zg_frags(const char* cur, int a_off, int b_off, int frag, float4 (&a)[MB],
                                          float4 (&bb)[2]) {
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) a[mb] = *reinterpret_cast<const float4*>(cur + a_off + mb * 32 * ZG_ROWB + frag);
+  for (int mb = 0; mb < MB; ++mb) a[mb] = *reinterpret_cast<const float4*>(cur + a_off + mb * 32 * ZG_ROWB + frag);
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) bb[nb] = *reinterpret_cast<const float4*>(cur + b_off + nb * 32 * ZG_ROWB + frag);
 }
 
-__device__ __forceinline__ void zg_mfmas(const float4 (&a)[4], const float4 (&bb)[2], floatx16 (&acc)[4][2]) {
+template <int MB>
+__device__ __forceinline__ void zg_mfmas(const float4 (&a)[MB], const float4 (&bb)[2], floatx16 (&acc)[MB][2]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma32(comp(a[mb], j), comp(bb[nb], j), acc[mb][nb]);
 }
@@ -74,15 +81,16 @@ __device__ __forceinline__ void zg_mfmas(const float4 (&a)[4], const float4 (&bb
 // the fragment reads of kq + 1 go out after the first 4 of kq's 32 MFMAs (pinned with
 // sched_group_barrier: left alone, hipcc put the reads after the MFMAs and waited for them);
 // by the next group's first MFMA they have long returned
-#define ZG_PIN_READS_THEN_MFMAS()                       \
-  __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  \
-  __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  \
-  __builtin_amdgcn_sched_group_barrier(0x008, 28, 0); \
+#define ZG_PIN_READS_THEN_MFMAS()                                 \
+  __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);            \
+  __builtin_amdgcn_sched_group_barrier(0x100, MB + 2, 0);       \
+  __builtin_amdgcn_sched_group_barrier(0x008, 8 * MB - 4, 0);   \
   __builtin_amdgcn_sched_barrier(0)
 
+template <int MB>
 __device__ __forceinline__ void zg_kstep(const char* cur, int a_off, int b_off, const int (&frag)[4],
-                                         floatx16 (&acc)[4][2]) {
-  float4 a0[4], b0[2], a1[4], b1[2];
+                                         floatx16 (&acc)[MB][2]) {
+  float4 a0[MB], b0[2], a1[MB], b1[2];
   zg_frags(cur, a_off, b_off, frag[0], a0, b0);
   __builtin_amdgcn_sched_barrier(0);
   zg_frags(cur, a_off, b_off, frag[1], a1, b1);
@@ -97,12 +105,15 @@ __device__ __forceinline__ void zg_kstep(const char* cur, int a_off, int b_off, 
   zg_mfmas(a1, b1, acc);
 }
 
+template <int BM>
 __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restrict__ W,
                                                             const float* __restrict__ X, int64_t ld, int N,
                                                             int C, int nv, float* __restrict__ Z, int tiles_m,
                                                             int tiles_n) {
-  __shared__ __attribute__((aligned(1024))) char lds0[ZG_BUFB];
-  __shared__ __attribute__((aligned(1024))) char lds1[ZG_BUFB];
+  using S = ZgShape<BM>;
+  constexpr int MB = S::MB, PPW = S::PPW;
+  __shared__ __attribute__((aligned(1024))) char lds0[S::BUFB];
+  __shared__ __attribute__((aligned(1024))) char lds1[S::BUFB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ldN = mixz_ldn(N);
   const int CN = C * ldN;
@@ -116,23 +127,23 @@ __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restr
   const int g = t / gsz, tin = t - g * gsz;
   const int gm = min(ZG_GROUP_M, tiles_m - g * ZG_GROUP_M);
   const int tm = g * ZG_GROUP_M + tin % gm, tn = tin / gm;
-  const int v0 = tm * ZG_BM, c0 = tn * ZG_BN;
+  const int v0 = tm * BM, c0 = tn * ZG_BN;
 
-  // ---- this lane's source rows for the wave's 12 pieces (clamped: rows past n_val and
+  // ---- this lane's source rows for the wave's PPW pieces (clamped: rows past n_val and
   //      columns past C*ldN / of padding clients load a valid row; the epilogue masks them) ----
-  const float* src[ZG_PPW];
+  const float* src[PPW];
   {
     const int rin = lane >> 3, slot = lane & 7;
 #pragma unroll
-    for (int i = 0; i < ZG_PPW; ++i) {
-      const int P = w * ZG_PPW + i;
-      if (P < ZG_BM / 8) {
+    for (int i = 0; i < PPW; ++i) {
+      const int P = w * PPW + i;
+      if (P < BM / 8) {
         const int r = 8 * P + rin;
         const int chunk = slot ^ ((r >> 1) & 7);
         const int v = min(v0 + r, nv - 1);
         src[i] = X + (int64_t)v * ld + chunk * 4;
       } else {
-        const int r = 8 * (P - ZG_BM / 8) + rin;
+        const int r = 8 * (P - BM / 8) + rin;
         const int chunk = slot ^ ((r >> 1) & 7);
         const int col = min(c0 + r, CN - 1);
         const int c = col / ldN;
@@ -147,12 +158,12 @@ __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restr
   int frag[4];
 #pragma unroll
   for (int kq = 0; kq < 4; ++kq) frag[kq] = lr * ZG_ROWB + (((2 * kq + h) ^ ((lr >> 1) & 7)) << 4);
-  const int a_off = (wm * 128) * ZG_ROWB;
-  const int b_off = ZG_ABYTES + (wn * 64) * ZG_ROWB;
+  const int a_off = (wm * (BM / 2)) * ZG_ROWB;
+  const int b_off = S::ABYTES + (wn * 64) * ZG_ROWB;
 
-  floatx16 acc[4][2];
+  floatx16 acc[MB][2];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -161,7 +172,7 @@ __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restr
   const int nk = (int)(ld / ZG_BK);     // even: ld is a multiple of 64
   // prologue: K-step 0 into buffer 0
 #pragma unroll
-  for (int i = 0; i < ZG_PPW; ++i) zg_glds(src[i], lds0 + w * ZG_PPW * 1024 + i * 1024);
+  for (int i = 0; i < PPW; ++i) zg_glds(src[i], lds0 + w * PPW * 1024 + i * 1024);
 
   // Two K-steps per iteration, one per buffer: each half reads one __shared__ array while the
   // other's pieces are in flight.  With both halves naming their arrays statically the
@@ -174,19 +185,19 @@ __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restr
     {
       const int64_t koff = (int64_t)(kt + 1) * ZG_BK;
 #pragma unroll
-      for (int i = 0; i < ZG_PPW; ++i) zg_glds(src[i] + koff, lds1 + w * ZG_PPW * 1024 + i * 1024);
+      for (int i = 0; i < PPW; ++i) zg_glds(src[i] + koff, lds1 + w * PPW * 1024 + i * 1024);
     }
     __builtin_amdgcn_sched_barrier(0);
-    zg_kstep(lds0, a_off, b_off, frag, acc);
+    zg_kstep<MB>(lds0, a_off, b_off, frag, acc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kt + 2 < nk) {
       const int64_t koff = (int64_t)(kt + 2) * ZG_BK;
 #pragma unroll
-      for (int i = 0; i < ZG_PPW; ++i) zg_glds(src[i] + koff, lds0 + w * ZG_PPW * 1024 + i * 1024);
+      for (int i = 0; i < PPW; ++i) zg_glds(src[i] + koff, lds0 + w * PPW * 1024 + i * 1024);
     }
     __builtin_amdgcn_sched_barrier(0);
-    zg_kstep(lds1, a_off, b_off, frag, acc);
+    zg_kstep<MB>(lds1, a_off, b_off, frag, acc);
   }
 
   // ---- epilogue: D[i][j] of a 32x32 block, reg r: i = (r&3) + 8 (r>>2) + 4 h, j = lane&31 ----
@@ -196,10 +207,10 @@ __global__ __launch_bounds__(256, 1) void mix_z_gemm_kernel(const float* __restr
     if (col >= CN) continue;
     const bool pad = (col % ldN) >= N;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int v = v0 + wm * 128 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int v = v0 + wm * (BM / 2) + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (v < nv) Z[(int64_t)v * CN + col] = pad ? 0.f : acc[mb][nb][r];
       }
   }
@@ -217,11 +228,22 @@ extern "C" int fs_mix_z(const float* d_W_all, const float* d_X_val, int64_t ld, 
   const int64_t CN = (int64_t)C * mixz_ldn(N);       // padded columns (zeros for n >= N)
   FS_REQUIRE(CN < (int64_t)1 << 30, "C * N too large");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int tiles_m = (n_val + ZG_BM - 1) / ZG_BM;
   const int tiles_n = (int)((CN + ZG_BN - 1) / ZG_BN);
-  FS_REQUIRE((int64_t)tiles_m * tiles_n < ((int64_t)1 << 31), "Z too large");
-  hipLaunchKernelGGL(mix_z_gemm_kernel, dim3(tiles_m * tiles_n), dim3(256), 0, st, d_W_all, d_X_val, ld, N, C, n_val,
-                     d_Z, tiles_m, tiles_n);
+  const int64_t t256 = (int64_t)((n_val + 255) / 256) * tiles_n;
+  FS_REQUIRE(t256 < ((int64_t)1 << 29), "Z too large");
+  int cus = 0, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (t256 >= (int64_t)cus) {          // 256-row tiles fill the chip (config 2: 400 tiles; as 800
+                                       // 128-row tiles 0.595 vs 0.55 ms, profiles/r04/z_gemm_time.txt)
+    const int tiles_m = (n_val + 255) / 256;
+    hipLaunchKernelGGL(mix_z_gemm_kernel<256>, dim3(tiles_m * tiles_n), dim3(256), 0, st, d_W_all, d_X_val, ld, N, C,
+                       n_val, d_Z, tiles_m, tiles_n);
+  } else {
+    const int tiles_m = (n_val + 127) / 128;
+    hipLaunchKernelGGL(mix_z_gemm_kernel<128>, dim3(tiles_m * tiles_n), dim3(256), 0, st, d_W_all, d_X_val, ld, N, C,
+                       n_val, d_Z, tiles_m, tiles_n);
+  }
   FS_LAUNCH_CHECK();
   return FS_OK;
 }

@@ -863,7 +863,6 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
   constexpr int NV4 = NK / 4;                      // float4 chunks per class and lane
   constexpr int KP = NK / 4;                       // clients a lane keeps after the row fold
   __shared__ __attribute__((aligned(16))) float gx[2][MQ_WAVES][64 * KP];
-  __shared__ __attribute__((aligned(16))) float gb[MQ_WAVES][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r = lane & 15;
@@ -978,9 +977,8 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
       const float ssum = row16_all<false>(real ? expf(o - m) : 0.f);                         \
       g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + expf(o - m - logf(ssum)) * invb : 0.f; \
     }                                                                                        \
-    gb[w][lane] = g;                                                                         \
-    float gv[CL];                                                                            \
-    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
+    float gv[CL];                  /* g of class c of this row: DPP row broadcast */         \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = row_get(g, c);                    \
     float2v gm2[NK / 2];                                                                      \
     _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = float2v{0.f, 0.f};            \
     _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
@@ -1723,7 +1721,6 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
   constexpr int NV4 = NK / 4;
   constexpr int KP = NK / 4;
   __shared__ __attribute__((aligned(16))) float gx[2][MQ_WAVES][64 * KP];
-  __shared__ __attribute__((aligned(16))) float gb[MQ_WAVES][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r = lane & 15;
@@ -1869,9 +1866,8 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     const float ssum = row16_all<false>(e);                                                  \
     const float g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + e * __builtin_amdgcn_rcpf(ssum) * invb \
                                         : 0.f;                                               \
-    gb[w][lane] = g;                                                                         \
-    float gv[CL];                                                                            \
-    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = gb[w][16 * q + c];                \
+    float gv[CL];                  /* g of class c of this row: DPP row broadcast */         \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = row_get(g, c);                    \
     float2v gm2[NK / 2];                                                                     \
     _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = float2v{0.f, 0.f};           \
     _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
@@ -1934,8 +1930,13 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
 }
 
 // clients per lane: 8 (128 per workgroup) for C <= 10, else 4 (r02s2qmc2: NK = 4, K = 16 at
-// N = 1000 measured the same 3.8 us per step as NK = 8, K = 8)
-static int qmc_nk(int C) { return C <= 10 ? 8 : 4; }
+// N = 1000 measured the same 3.8 us per step as NK = 8, K = 8); fs_tuning.mix_qmc_lane_clients
+// forces one
+static int qmc_nk(int C) {
+  const int f = tuning().mix_qmc_lane_clients;
+  if (f == 4 || C > 10) return 4;
+  return 8;
+}
 
 static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
   const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
@@ -1988,8 +1989,7 @@ extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   const int S = mc_slice(N);
   const int K = S ? (mix_ldn(N) + S - 1) / S : 0;
   const int64_t mc = mc_covers(N, C, Bv) ? mc_xbytes(K) : 0;
-  const int nk = qmc_nk(C);
-  const int64_t qmc = mc_xbytes((mix_ldn(N) + 16 * nk - 1) / (16 * nk));
+  const int64_t qmc = mc_xbytes((mix_ldn(N) + 63) / 64);   // the larger K of either lane width
   return std::max(mc, (N > 128 && C <= 16 && Bv <= 16) ? qmc : (int64_t)0) + MC_ERR_BYTES;
 }
 

@@ -134,3 +134,25 @@ def test_sharded_matches_single_process(algo):
         np.testing.assert_allclose(res[0], ref[0], atol=1e-5)
         np.testing.assert_allclose(res[1], ref[1], atol=1e-5)
         assert np.abs(res[2] - ref[2]).max() <= 100.0 / 70 + 1e-4
+
+
+def test_bench_two_ranks_launcher():
+    """The launcher the driver's 8-GPU node runs: ``bench.py --gpus 2`` starts two workers of
+    itself (no torchrun), here over gloo on the box's one GPU (FS_BENCH_BACKEND=gloo: the RCCL
+    path needs a GPU per rank), and relays rank 0's line: n_gpus and the dist object come from
+    the process group, the checked all-reduce of rank + 1 gives 3."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FS_BENCH_BACKEND='gloo', HSA_ENABLE_IPC_MODE_LEGACY='0')
+    env.pop('WORLD_SIZE', None)
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--config', '2', '--steps', '2',
+                        '--warmup', '1', '--no-legs', '--no-cpu-baseline', '--no-fedamw-leg'],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line['n_gpus'] == 2
+    assert line['dist']['world_size'] == 2 and line['dist']['backend'] == 'gloo'
+    assert line['dist']['allreduce_check'] == 3.0
+    assert line['value'] > 0 and line['config']['clients_total'] == 200

@@ -544,19 +544,22 @@ def test_mix_solve_multi_cu(amd, N, C, nv, Bv):
     assert mode == 2, mode             # the multi-CU solver ran (a timed-out spin raises in check_errors)
 
 
-@pytest.mark.parametrize('h', [-1, 16])
+@pytest.mark.parametrize('h,lc', [(-1, 0), (16, 0), (16, 4)])
 @pytest.mark.parametrize('N,C,nv,Bv', [
-    (1000, 10, 97, 16),     # config 5 client count: K = 8 workgroups of 128 clients
+    (1000, 10, 97, 16),     # config 5 client count: K = 8 workgroups of 128 clients (lc = 4: 16 of 64)
     (300, 4, 60, 16),       # K = 3, ragged last slice
     (129, 3, 77, 8),        # K = 2, Bv < 16, ragged last batch
     (2000, 2, 45, 16),      # K = 16
     (1000, 16, 40, 16),     # C = 16: 64 clients per workgroup, K = 16
     (200, 10, 133, 16),     # K = 2
 ])
-def test_mix_solve_qmc(amd, N, C, nv, Bv, h):
+def test_mix_solve_qmc(amd, N, C, nv, Bv, h, lc):
     """fs_mix_solve's multi-CU quarter-wave solver (clients over K workgroups, one exchange of
-    the partial logits per step; without / with L2 prefetch helpers) vs the oracle's p-SGD."""
-    with amd.lib.tuning(mix_solver='qmc', mix_prefetch=h):
+    the partial logits per step; without / with L2 prefetch helpers; lc = 4: the 4-clients-per-
+    lane instance forced, twice the workgroups) vs the oracle's p-SGD."""
+    if lc == 4 and (N + 3) // 4 * 4 > 16 * 64:
+        pytest.skip('K = ceil(N / 64) > 16 workgroups: not a qmc shape at 4 clients per lane')
+    with amd.lib.tuning(mix_solver='qmc', mix_prefetch=h, mix_qmc_lane_clients=lc):
         test_mix_solve_variants(amd, N, C, nv, Bv, lr=0.05 if N >= 1000 else 0.5)   # (see test_mix_solve_multi_cu)
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
 
@@ -665,12 +668,13 @@ def test_mix_solve_forced_fallbacks(amd, solver, N, C):
 
 
 @pytest.mark.parametrize('N,C,D,nv', [(1, 1, 64, 1), (3, 2, 64, 255), (23, 5, 192, 257), (100, 10, 2048, 700),
-                                      (130, 7, 320, 513), (300, 4, 128, 1000)])
+                                      (130, 7, 320, 513), (300, 4, 128, 1000), (998, 4, 64, 4097)])
 def test_mix_z_shapes(amd, N, C, D, nv):
-    """fs_mix_z (mix_z.hip: 256 x 128 tiles, K-steps of 32, LDS-DMA images) against fp64 on
-    ragged shapes: row tails (n_val mod 256), column tails (C * ldN mod 128), padding clients
-    (N mod 4), the shortest K (ld = 64: one loop iteration); padding columns exactly 0 and
-    nothing written past Z (a guard row after it)."""
+    """fs_mix_z (mix_z.hip: 128- or 256-row x 128 tiles, K-steps of 32, LDS-DMA images) against
+    fp64 on ragged shapes: row tails (n_val mod 128 / 256), column tails (C * ldN mod 128),
+    padding clients (N mod 4), the shortest K (ld = 64: one loop iteration); the last shape
+    (544 tiles of 256 rows) takes the 256-row form, the others the 128-row form; padding columns
+    exactly 0 and nothing written past Z (a guard row after it)."""
     rs = np.random.RandomState(N + nv)
     ld = (D + 63) // 64 * 64
     ldN = (N + 3) // 4 * 4
