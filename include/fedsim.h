@@ -80,8 +80,8 @@ const char* fs_last_error(void);
  *                      first SP_E1 (local_train_split.hip: 4 at G = 2, 6 at G >= 4) of each
  *                      wave's 16 next-step row loads right after the hand-off (they stream
  *                      through the softmax), -1 = all of them inside the backward
- *   mix_qmc_lane_clients (ABI 13) qmc p-solver: clients per lane, 0 = by shape (8 for
- *                      C <= 10, else 4), 4 = force 4 (K = ceil(N / 64) workgroups, <= 16),
+ *   mix_qmc_lane_clients (ABI 13) qmc p-solver: clients per lane, 0 = by shape (4 where
+ *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
  *                      of the K-partial sums (a different client-to-workgroup split)
  * ------------------------------------------------------------------------- */

@@ -1689,14 +1689,15 @@ static int mix_solve_mc(hipStream_t st, const float* Z, const int32_t* y, const 
 
 // ----------------------------------------------------------------------------
 // p-solve, multi-CU quarter-wave form "qmc" (Bv <= 16, 128 < N <= 16 * 16 * NK, C <= CL):
-// the quarter-wave layout on K <= 16 workgroups of 16*NK clients each (N = 1000: K = 8),
+// the quarter-wave layout on K <= 16 workgroups of 16*NK clients each (N = 1000: K = 16 of 64),
 // all on one XCD.  A workgroup computes its clients' partial logits, publishes them (the
 // 16 x C row/class values, 8-byte {tag, value} granules) and reads the K partials of every
 // value back -- ONE hop -- summing them in workgroup order, so every workgroup holds the
 // bitwise-same logits, softmax and CE gradient; the gradient of its own clients, the
 // momentum step and p stay local (no second hop).  Its 16 x C x 16NK Z values per step come
 // from L2, where H helper workgroups on the same XCD prefetch the rows of the next steps
-// (FS_MIX_PF_H, default 16 for this solver).  Spins are bounded; a timeout sets the error
+// (fs_tuning.mix_prefetch; by default 24, at most the 32 - K CUs left on the XCD, 6 steps
+// ahead).  Spins are bounded; a timeout sets the error
 // word and poisons p with NaN.
 // ----------------------------------------------------------------------------
 constexpr int QMC_KMAX = 16;
@@ -1929,18 +1930,22 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
   }
 }
 
-// clients per lane: 8 (128 per workgroup) for C <= 10, else 4 (r02s2qmc2: NK = 4, K = 16 at
-// N = 1000 measured the same 3.8 us per step as NK = 8, K = 8); fs_tuning.mix_qmc_lane_clients
-// forces one
-static int qmc_nk(int C) {
+// clients per lane: 4 (64 per workgroup) wherever K = ceil(N / 64) <= 16 workgroups, else 8
+// (C <= 10 only).  Round 4 (profiles/r04/qmc_lane_ab*.txt, us per step, 8 vs 4): N = 1000
+// C = 10 3.60-3.71 vs 3.30; N = 300 3.00 vs 2.50; N = 520 3.23 vs 2.73 -- half the gather per CU
+// outweighs the hop's 16 partners since the hop re-polls all missing partners at once (round 2,
+// polling them one after another, measured the two the same).  fs_tuning.mix_qmc_lane_clients
+// forces one.
+static int qmc_nk(int N, int C) {
   const int f = tuning().mix_qmc_lane_clients;
-  if (f == 4 || C > 10) return 4;
-  return 8;
+  if (C > 10 || f == 4) return 4;
+  if (f == 8) return 8;
+  return (mix_ldn(N) + 63) / 64 <= QMC_KMAX ? 4 : 8;
 }
 
 static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
   const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
-  const int nk = qmc_nk(C);
+  const int nk = qmc_nk(N, C);
   return Bv <= 16 && N > 128 && C <= 16 && (mix_ldn(N) + 16 * nk - 1) / (16 * nk) <= QMC_KMAX &&
          zb < ((int64_t)1 << 31) && (int64_t)epochs * nv < ((int64_t)1 << 31);
 }
@@ -1951,7 +1956,7 @@ static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const
                          int64_t ws_bytes, MixPrefetch pf, int zR = 1) {
   if (!qmc_covers(N, C, Bv, nv, epochs)) return 1;
   const int zL = mix_ldn(N) / zR;
-  const int nk = qmc_nk(C);
+  const int nk = qmc_nk(N, C);
   const int K = (mix_ldn(N) + 16 * nk - 1) / (16 * nk);
   const int64_t xbytes = mc_xbytes(K);
   if (!d_ws || ws_bytes < xbytes + MC_ERR_BYTES)
