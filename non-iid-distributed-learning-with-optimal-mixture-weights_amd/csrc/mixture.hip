@@ -280,6 +280,62 @@ __device__ __forceinline__ void momentum_step(float& p, float& b, float g, int f
   p = p + (-lr) * nb;                         // p.add_(buf, alpha=-lr)
 }
 
+// the same step where lane condition `live` holds, p and b unchanged elsewhere (selects, no
+// branch: the quarter-wave solvers' padding clients)
+__device__ __forceinline__ void momentum_step_sel(float& p, float& b, float g, int first, float mom, float lr,
+                                                  bool live) {
+  float np = p, nb = b;
+  momentum_step(np, nb, g, first, mom, lr);
+  p = live ? np : p;
+  b = live ? nb : b;
+}
+
+// max over the 16 lanes of a DPP row, one v_max_f32_dpp per level (hipcc's fmaxf over a DPP
+// move costs a move, a canonicalising max and the max per level); every lane of the row ends
+// with the same value.  Inputs are finite or -inf.
+__device__ __forceinline__ float row16_max(float x) {
+  float r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "=&v"(r)
+      : "v"(x));
+  return r;
+}
+
+// rs_bank<8> on the 8 pairs (v[i], v[i + 8]) and then rs_bank<4> on (v[i], v[i + 4]), i.e. the
+// first two reduce-scatter levels of the quarter-wave solvers' 16 class partials, as two asm
+// blocks with ONE hazard pad each (rs_bank pads every call: 12 x s_nop 1 per step).  Every DPP
+// read in a block is of a block input, written before the block's pad; outputs are early-clobber.
+__device__ __forceinline__ void rs_banks_8_4(float (&v)[16]) {
+#define RSB8(o, a, b)                                                                        \
+  "v_add_f32_dpp " o ", " a ", " a " row_ror:8 row_mask:0xf bank_mask:0x3\n\t"             \
+  "v_add_f32_dpp " o ", " b ", " b " row_ror:8 row_mask:0xf bank_mask:0xc\n\t"
+#define RSB4(o, a, b)                                                                        \
+  "v_add_f32_dpp " o ", " a ", " a " row_shl:4 row_mask:0xf bank_mask:0x5\n\t"             \
+  "v_add_f32_dpp " o ", " b ", " b " row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+  float w[8];
+  asm volatile("s_nop 1\n\t" RSB8("%0", "%8", "%16") RSB8("%1", "%9", "%17") RSB8("%2", "%10", "%18")
+               RSB8("%3", "%11", "%19") RSB8("%4", "%12", "%20") RSB8("%5", "%13", "%21")
+               RSB8("%6", "%14", "%22") RSB8("%7", "%15", "%23")
+               : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]),
+                 "=&v"(w[7])
+               : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+                 "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+  asm volatile("s_nop 1\n\t" RSB4("%0", "%4", "%8") RSB4("%1", "%5", "%9") RSB4("%2", "%6", "%10")
+               RSB4("%3", "%7", "%11")
+               : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+               : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]));
+#undef RSB8
+#undef RSB4
+}
+
 constexpr int MR_WAVES = 16;
 
 // Diagnostic build only (-DFS_MIX_STAMPS, `make stamps`): per-phase cycle sums of wave 0,
@@ -945,28 +1001,26 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     const int bc = min(Bv, nv - csb * Bv);                                                   \
     csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
     float v[16];                                                                             \
-    _Pragma("unroll") for (int c = 0; c < 16; ++c) {                                         \
-      float a = 0.f;                                                                         \
-      if (c < CL) {                                                                          \
-        /* packed pairs (v_pk_fma_f32): even and odd clients summed apart, then joined */    \
-        float2v a2 = {0.f, 0.f};                                                             \
-        _Pragma("unroll") for (int j = 0; j < NK; j += 2) a2 = __builtin_elementwise_fma(   \
-            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2);          \
-        a = a2.x + a2.y;                                                                     \
+    {              /* packed pairs (v_pk_fma_f32): even and odd clients summed apart, then    \
+                      joined; the classes' chains interleaved (independent accumulators) */   \
+      float2v a2[CL];                                                                        \
+      _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = float2v{0.f, 0.f};              \
+      _Pragma("unroll") for (int j = 0; j < NK; j += 2) {                                    \
+        _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = __builtin_elementwise_fma(   \
+            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2[c]);      \
       }                                                                                      \
-      v[c] = a;                                                                              \
+      _Pragma("unroll") for (int c = 0; c < 16; ++c) v[c] = c < CL ? a2[c].x + a2[c].y : 0.f; \
     }                                                                                        \
     MR_STAMP(1)                                                                              \
     /* the late classes of step s - 1 + DEPTH (its early ones went out with the last step) */ \
     if constexpr (SPL < CL) {                                                                \
       if (s > 0) MQ_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
     }                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) v[i] = rs_bank<8>(v[i], v[i + 8]);         \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) v[i] = rs_bank<4>(v[i], v[i + 4]);         \
+    rs_banks_8_4(v);                                                                         \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
     const float o = rs_pair(v[0], v[1], 1, lane);  /* class r's logit */                     \
     const bool real = r < C;                                                                 \
-    const float m = row16_all<true>(real ? o : -INFINITY);                                   \
+    const float m = row16_max(real ? o : -INFINITY);                                         \
     const float invb = bc == Bv ? invB : invT;                                               \
     float g;                                                                                 \
     if constexpr (FASTX) {         /* v_exp_f32 / v_rcp_f32: softmax = e / sum */            \
@@ -1010,7 +1064,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
       float gs = gx[par][0][lane * KP + i];                                                  \
       _Pragma("unroll") for (int k = 1; k < MQ_WAVES; ++k) gs += gx[par][k][lane * KP + i];  \
-      if (n0 + kj0 + i < N) momentum_step(po[i], bo[i], gs, first, mom, lr);                 \
+      momentum_step_sel(po[i], bo[i], gs, first, mom, lr, n0 + kj0 + i < N);                 \
     }                                                                                        \
     first = 0;                                                                               \
     /* all-gather p back to NK clients per lane */                                           \
@@ -1807,18 +1861,17 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     const int bc = min(Bv, nv - csb * Bv);                                                   \
     csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
     float v[16];                                                                             \
-    _Pragma("unroll") for (int c = 0; c < 16; ++c) {                                         \
-      float a = 0.f;                                                                         \
-      if (c < CL) {                                                                          \
-        float2v a2 = {0.f, 0.f};                                                             \
-        _Pragma("unroll") for (int j = 0; j < NK; j += 2) a2 = __builtin_elementwise_fma(   \
-            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2);          \
-        a = a2.x + a2.y;                                                                     \
+    {              /* packed pairs (v_pk_fma_f32): even and odd clients summed apart, then    \
+                      joined; the classes' chains interleaved (independent accumulators) */   \
+      float2v a2[CL];                                                                        \
+      _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = float2v{0.f, 0.f};              \
+      _Pragma("unroll") for (int j = 0; j < NK; j += 2) {                                    \
+        _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = __builtin_elementwise_fma(   \
+            half2(zr[R_][c][j >> 2], (j >> 1) & 1), float2v{pr[j], pr[j + 1]}, a2[c]);      \
       }                                                                                      \
-      v[c] = a;                                                                              \
+      _Pragma("unroll") for (int c = 0; c < 16; ++c) v[c] = c < CL ? a2[c].x + a2[c].y : 0.f; \
     }                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) v[i] = rs_bank<8>(v[i], v[i + 8]);         \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) v[i] = rs_bank<4>(v[i], v[i + 4]);         \
+    rs_banks_8_4(v);                                                                         \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
     const float opart = rs_pair(v[0], v[1], 1, lane);   /* this workgroup's share */         \
     MR_STAMP(1)                                                                              \
@@ -1861,7 +1914,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     if constexpr (SPL < CL) {                                                                \
       if (s > 0) QM_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
     }                                                                                        \
-    const float m = row16_all<true>(real ? o : -INFINITY);                                   \
+    const float m = row16_max(real ? o : -INFINITY);                                         \
     const float invb = bc == Bv ? invB : invT;                                               \
     const float e = real ? __expf(o - m) : 0.f;                                              \
     const float ssum = row16_all<false>(e);                                                  \
@@ -1897,7 +1950,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
       float gs = gx[par][0][lane * KP + i];                                                  \
       _Pragma("unroll") for (int kk = 1; kk < MQ_WAVES; ++kk) gs += gx[par][kk][lane * KP + i]; \
-      if (n0 + kj0 + i < N) momentum_step(po[i], bo[i], gs, first, mom, lr);                 \
+      momentum_step_sel(po[i], bo[i], gs, first, mom, lr, n0 + kj0 + i < N);                 \
     }                                                                                        \
     first = 0;                                                                               \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \

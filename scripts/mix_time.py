@@ -1,6 +1,6 @@
 """Diagnostic: fs_mix_solve time per dependent p-SGD step (and fs_mix_z) at a given shape.
     [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] [FS_MIX_PF_H=h] [FS_MIX_PF_LEAD=l] [FS_MIX_QMC_LC=4|8]
-    python scripts/mix_time.py
+    [FS_MIX_DUMP=file.npy (p and buf after the run, for bitwise A/B of two builds)] python scripts/mix_time.py
         [N] [C] [n_val] [epochs] [D]
 (GPU box; default config 2; the variables only select fs_tuning fields for this run)"""
 import os
@@ -55,6 +55,8 @@ print('N=%d C=%d n_val=%d epochs=%d: mix_z %.1f us (%.1f TFLOP/s), mix_solve %.2
       'p finite: %s' % (N, C, nv, ep, zms * 1e3, 2.0 * N * C * D * nv / zms / 1e9, sms, sms * 1e3 / steps, steps,
                         bool(torch.isfinite(mix.p).all())), flush=True)
 mix.check_errors()
+if os.environ.get('FS_MIX_DUMP'):
+    np.save(os.environ['FS_MIX_DUMP'], np.stack([mix.p[:N].cpu().numpy(), mix.buf[:N].cpu().numpy()]))
 print('  solver requested %s, ran %s' % (SOLVER,
                                          L.SOLVER_NAMES[L.lib().fs_mix_solve_last_mode()]), flush=True)
 if STAMPS:
