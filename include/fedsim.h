@@ -84,6 +84,10 @@ const char* fs_last_error(void);
  *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
  *                      of the K-partial sums (a different client-to-workgroup split)
+ *   mix_quad_loaders   (ABI 13) quad p-solver at 64 < N <= 128, C <= 10 (config 2): 0 = with
+ *                      4 loader waves that stream the late classes' Z rows into LDS (default),
+ *                      -1 = without (each compute wave issues all of its loads); bitwise the
+ *                      same p
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -107,6 +111,7 @@ typedef struct fs_tuning {
   int train_form;
   int split_early;
   int mix_qmc_lane_clients;
+  int mix_quad_loaders;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);

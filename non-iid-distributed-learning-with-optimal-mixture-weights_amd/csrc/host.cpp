@@ -51,6 +51,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": split_early must be -1 or 0");
   if (t && t->mix_qmc_lane_clients != 0 && t->mix_qmc_lane_clients != 4 && t->mix_qmc_lane_clients != 8)
     return fail(FS_EINVAL, std::string(fn) + ": mix_qmc_lane_clients must be 0, 4 or 8");
+  if (t && (t->mix_quad_loaders < -1 || t->mix_quad_loaders > 0))
+    return fail(FS_EINVAL, std::string(fn) + ": mix_quad_loaders must be -1 or 0");
   return FS_OK;
 }
 

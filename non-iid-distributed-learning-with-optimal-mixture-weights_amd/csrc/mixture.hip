@@ -336,6 +336,35 @@ __device__ __forceinline__ void rs_banks_8_4(float (&v)[16]) {
 #undef RSB4
 }
 
+// M permlane swaps (lane distance OFF = 32 or 16) of the pairs (a[i], b[i]) behind ONE hazard
+// pad (rs_level / gather_pair pad every swap); the pairs are distinct registers, so no swap of
+// the batch reads another's result
+template <int OFF, int M>
+__device__ __forceinline__ void swap_batch(float (&a)[M], float (&b)[M]) {
+  static_assert((OFF == 32 || OFF == 16) && (M == 1 || M == 2 || M == 4), "swap batch");
+  if constexpr (OFF == 32) {
+    if constexpr (M == 1)
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a[0]), "+v"(b[0]));
+    else if constexpr (M == 2)
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
+                   : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+    else
+      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %4\n\tv_permlane32_swap_b32 %1, %5\n\t"
+                   "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %3, %7"
+                   : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+  } else {
+    if constexpr (M == 1)
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a[0]), "+v"(b[0]));
+    else if constexpr (M == 2)
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                   : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+    else
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %4\n\tv_permlane16_swap_b32 %1, %5\n\t"
+                   "v_permlane16_swap_b32 %2, %6\n\tv_permlane16_swap_b32 %3, %7"
+                   : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]));
+  }
+}
+
 constexpr int MR_WAVES = 16;
 
 // Diagnostic build only (-DFS_MIX_STAMPS, `make stamps`): per-phase cycle sums of wave 0,
@@ -895,6 +924,14 @@ static bool mix_solve_reg2(hipStream_t st, const float* Z, const int32_t* y, con
 // Optional L2 prefetch helpers as for the register solver (FS_MIX_PF_H).
 // ----------------------------------------------------------------------------
 constexpr int MQ_WAVES = 4;
+// Diagnostic build only (`make probe`, -DFS_MIX_PROBE_NOLOAD): the quarter-wave solver skips
+// its in-loop Z loads (the ring keeps its first rows: wrong p, timing only) -- what a step costs
+// without the vector-memory issue.  Never in the shipped library.
+#ifdef FS_MIX_PROBE_NOLOAD
+constexpr bool kMixProbeNoLoad = true;
+#else
+constexpr bool kMixProbeNoLoad = false;
+#endif
 
 typedef float float2v __attribute__((ext_vector_type(2)));
 // elements (2h, 2h+1) of a float4
@@ -1013,7 +1050,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     }                                                                                        \
     MR_STAMP(1)                                                                              \
     /* the late classes of step s - 1 + DEPTH (its early ones went out with the last step) */ \
-    if constexpr (SPL < CL) {                                                                \
+    if constexpr (SPL < CL && !kMixProbeNoLoad) {                                            \
       if (s > 0) MQ_ISSUE((R_ + DEPTH - 1) % DEPTH, late_row, SPL, CL);                      \
     }                                                                                        \
     rs_banks_8_4(v);                                                                         \
@@ -1047,15 +1084,31 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     MR_STAMP(2)                                                                              \
     /* slot consumed: refill with step s + DEPTH, then fetch the rows of s + 2 DEPTH */      \
     labq[R_] = y[idxq[R_]];                                                                  \
-    MQ_ISSUE(R_, idxq[R_], 0, SPL);                                                          \
+    if constexpr (!kMixProbeNoLoad) MQ_ISSUE(R_, idxq[R_], 0, SPL);                          \
     late_row = idxq[R_];                                                                     \
     idxq[R_] = fetch_row();                                                                  \
     MR_STAMP(6)                                                                              \
     /* fold the wave's 4 rows: reduce-scatter over the row groups */                         \
-    float t[NK / 2];                                                                         \
-    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = rs_level<32, true>(gme[i], gme[i + NK / 2], lane); \
+    float t[NK / 2];               /* = rs_level<32> / <16>, one pad per level */            \
+    {                                                                                        \
+      float sa[NK / 2], sb[NK / 2];                                                          \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        sa[i] = gme[i];                                                                      \
+        sb[i] = gme[i + NK / 2];                                                             \
+      }                                                                                      \
+      swap_batch<32, NK / 2>(sa, sb);                                                        \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = sa[i] + sb[i];               \
+    }                                                                                        \
     float u[KP];                                                                             \
-    _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = rs_level<16, true>(t[i], t[i + KP], lane); \
+    {                                                                                        \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        sa[i] = t[i];                                                                        \
+        sb[i] = t[i + KP];                                                                   \
+      }                                                                                      \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = sa[i] + sb[i];                   \
+    }                                                                                        \
     const int par = s & 1;                                                                   \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
     MR_STAMP(3)                                                                              \
@@ -1068,8 +1121,22 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
     }                                                                                        \
     first = 0;                                                                               \
     /* all-gather p back to NK clients per lane */                                           \
-    _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \
-    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
+    {                              /* = gather_pair<16> / <32>, one pad per level */         \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) sa[i] = sb[i] = po[i];                  \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        t[i] = sa[i];                                                                        \
+        t[i + KP] = sb[i];                                                                   \
+      }                                                                                      \
+      float ga[NK / 2], gb2[NK / 2];                                                         \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) ga[i] = gb2[i] = t[i];              \
+      swap_batch<32, NK / 2>(ga, gb2);                                                       \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        pr[i] = ga[i];                                                                       \
+        pr[i + NK / 2] = gb2[i];                                                             \
+      }                                                                                      \
+    }                                                                                        \
     MR_STAMP(5)                                                                              \
     ++s;                                                                                     \
     if (pf_prog && (s & 3) == 0) mix_publish_progress(pf_prog, s);                           \
@@ -1104,6 +1171,271 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
 template <int CL>
 constexpr int quad_split() { return (3 * CL + 9) / 10; }
 
+// ----------------------------------------------------------------------------
+// The quarter-wave solver with LOADER WAVES (round 4, fs_tuning.mix_quad_loaders).  The
+// no-load probe (`make probe`, profiles/r04/quad_noload_probe.txt) put a third of quad's step
+// at config 2 in issuing its Z loads: 20 buffer_load_dwordx4 per wave per step, ~40 cycles
+// each, in the compute waves' own instruction stream (1.25 -> 0.87 us per step without them).
+// Here 4 more waves (one per SIMD) issue the late classes' loads as LDS-DMA
+// (global_load_lds_dwordx4, 1 KB per instruction, the lane layout of the register ring) into a
+// 2-slot LDS ring: loader L serves compute wave L's 4 rows.  Step s's slot is filled after the
+// workgroup barrier of step s - 2 (whose compute waves had read it) and landed (vmcnt(0)) before
+// the barrier of step s - 1; the compute waves read it with ds_read_b128 at step s.  The early
+// classes stay in the compute waves' register ring as in quad.  Same values into the same
+// arithmetic: bitwise quad's p (tests/test_gpu_parity.py).  Lanes past ldN (padding clients,
+// p = 0 and never stepped) read column 0 instead of zeros: finite values times p = 0.
+// ----------------------------------------------------------------------------
+template <int NK, int CL, int SPL>
+__global__ __launch_bounds__(2 * MQ_WAVES * 64) void mix_solve_quadl_kernel(
+    const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
+    int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
+    int* __restrict__ first_flag, int z_bytes, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead) {
+  static_assert(NK == 4 || NK == 8, "clients per lane");
+  static_assert(SPL >= 1 && SPL < CL && CL <= 16, "classes");
+  constexpr int DEPTH = 2;
+  constexpr int NV4 = NK / 4;
+  constexpr int KP = NK / 4;
+  constexpr int CLL = CL - SPL;                    // late classes, through LDS
+  static_assert(DEPTH * MQ_WAVES * CLL * NV4 * 1024 <= 128 * 1024, "LDS ring");
+  if (blockIdx.x != 0) {                           // L2 prefetch helpers (speed only)
+    if (pf_prog && blockIdx.x % 8 == 0)
+      mix_prefetch_helper(Z, perms, N, C, nv, epochs, Bv, blockIdx.x / 8 - 1, pf_h, pf_lead, pf_prog);
+    return;
+  }
+  __shared__ __attribute__((aligned(1024))) char lz[DEPTH][MQ_WAVES][CLL][NV4][1024];
+  __shared__ __attribute__((aligned(16))) float gx[2][MQ_WAVES][64 * KP];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int w = wv & (MQ_WAVES - 1);               // compute wave w, or the loader of wave w's rows
+  const int q = lane >> 4, r = lane & 15;
+  const int brow = MQ_WAVES * w + q;
+  const int ldN = mix_ldn(N);
+  const int CN = C * ldN;
+  const int nbat = (nv + Bv - 1) / Bv;
+  const int total = epochs * nbat;
+  const int n0 = NK * r;
+  int fst = 0, fep = 0, fsb = 0;
+  auto fetch_row = [&]() -> int {
+    const int base = fep * nv + fsb * Bv;
+    const int bc = min(Bv, nv - fsb * Bv);
+    const int row = perms[base + (brow < bc ? brow : 0)];
+    if (fst + 1 < total) {
+      ++fst;
+      if (++fsb == nbat) {
+        fsb = 0;
+        ++fep;
+      }
+    }
+    return row;
+  };
+  if (wv >= MQ_WAVES) {
+    // ---- loader wave: the late classes of its compute wave's rows, two steps ahead ----
+    int cofs[NV4];
+#pragma unroll
+    for (int h = 0; h < NV4; ++h) cofs[h] = n0 + 4 * h < ldN ? n0 + 4 * h : 0;
+    auto issue = [&](int slot, int row) {
+      const float* zrow = Z + (int64_t)row * CN;
+#pragma unroll
+      for (int c = 0; c < CLL; ++c) {
+        const int cc = min(c + SPL, C - 1);
+#pragma unroll
+        for (int h = 0; h < NV4; ++h)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(zrow + cc * ldN + cofs[h]),
+                                           (__attribute__((address_space(3))) void*)&lz[slot][w][c][h][0], 16, 0, 0);
+      }
+    };
+    issue(0, fetch_row());
+    issue(1, fetch_row());
+    int next = fetch_row();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                  // B_init: slots 0 and 1 landed
+    for (int s = 0; s < total; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step s + 1's slot landed
+      __builtin_amdgcn_s_barrier();                // B_s: the compute waves are done with slot s & 1
+      asm volatile("" ::: "memory");
+      if (s + 2 < total) {
+        issue(s & 1, next);
+        next = fetch_row();
+      }
+    }
+    return;
+  }
+  // ---- compute wave: quad's step, the late classes from the LDS ring ----
+  float pr[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) pr[j] = n0 + j < N ? p[n0 + j] : 0.f;
+  const int kj0 = (q >> 1) * (NK / 2) + (q & 1) * (NK / 4);
+  float po[KP], bo[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    const int n = n0 + kj0 + i;
+    po[i] = n < N ? p[n] : 0.f;
+    bo[i] = n < N ? buf[n] : 0.f;
+  }
+  int first = *first_flag;
+  const float invB = 1.0f / (float)Bv;
+  const float invT = 1.0f / (float)(nv - (nbat - 1) * Bv);
+  uint32_t lofs[NV4];
+#pragma unroll
+  for (int h = 0; h < NV4; ++h) lofs[h] = n0 + 4 * h < ldN ? 4u * (uint32_t)(n0 + 4 * h) : 0x80000000u;
+  int sofs[SPL];
+#pragma unroll
+  for (int c = 0; c < SPL; ++c) sofs[c] = __builtin_amdgcn_readfirstlane(4 * min(c, C - 1) * ldN);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Z), 0, z_bytes, 0x00020000);
+  floatx4 zr[DEPTH][SPL][NV4];
+  int idxq[DEPTH], labq[DEPTH];
+#define QL_ISSUE(R_, ROW_)                                                                   \
+  {                                                                                          \
+    const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
+    _Pragma("unroll") for (int c = 0; c < SPL; ++c) {                                        \
+      _Pragma("unroll") for (int h = 0; h < NV4; ++h) zr[R_][c][h] = __builtin_bit_cast(     \
+          floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[h], sofs[c], 0));   \
+    }                                                                                        \
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) {
+    const int row = fetch_row();
+    labq[k] = y[row];
+    QL_ISSUE(k, row);
+  }
+#pragma unroll
+  for (int k = 0; k < DEPTH; ++k) idxq[k] = fetch_row();
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __builtin_amdgcn_s_barrier();                    // B_init
+  asm volatile("" ::: "memory");
+  int csb = 0;
+  int s = 0;
+#ifdef FS_MIX_STAMPS
+  unsigned long long mr_acc[6] = {0, 0, 0, 0, 0, 0}, mr_prev = 0;
+#endif
+#define QL_STEP(R_)                                                                          \
+  {                                                                                          \
+    if (s >= total) break;                                                                   \
+    MR_STAMP(0)                                                                              \
+    floatx4 zl[CLL][NV4];          /* the late classes of this step, from the LDS ring */   \
+    _Pragma("unroll") for (int c = 0; c < CLL; ++c) {                                        \
+      _Pragma("unroll") for (int h = 0; h < NV4; ++h)                                        \
+        zl[c][h] = *reinterpret_cast<const floatx4*>(&lz[R_][w][c][h][lane * 16]);           \
+    }                                                                                        \
+    const int bc = min(Bv, nv - csb * Bv);                                                   \
+    csb = csb + 1 == nbat ? 0 : csb + 1;                                                     \
+    float v[16];                                                                             \
+    {                                                                                        \
+      float2v a2[CL];                                                                        \
+      _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = float2v{0.f, 0.f};              \
+      _Pragma("unroll") for (int j = 0; j < NK; j += 2) {                                    \
+        _Pragma("unroll") for (int c = 0; c < CL; ++c) a2[c] = __builtin_elementwise_fma(   \
+            half2(c < SPL ? zr[R_][c < SPL ? c : 0][j >> 2] : zl[c < SPL ? 0 : c - SPL][j >> 2], \
+                  (j >> 1) & 1),                                                             \
+            float2v{pr[j], pr[j + 1]}, a2[c]);                                               \
+      }                                                                                      \
+      _Pragma("unroll") for (int c = 0; c < 16; ++c) v[c] = c < CL ? a2[c].x + a2[c].y : 0.f; \
+    }                                                                                        \
+    MR_STAMP(1)                                                                              \
+    rs_banks_8_4(v);                                                                         \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) v[i] = rs_pair(v[i], v[i + 2], 2, lane);   \
+    const float o = rs_pair(v[0], v[1], 1, lane);                                            \
+    const bool real = r < C;                                                                 \
+    const float m = row16_max(real ? o : -INFINITY);                                         \
+    const float invb = bc == Bv ? invB : invT;                                               \
+    const float e = real ? __expf(o - m) : 0.f;                                              \
+    const float ssum = row16_all<false>(e);                                                  \
+    const float g = (real && brow < bc) ? (r == labq[R_] ? -invb : 0.f) + e * __builtin_amdgcn_rcpf(ssum) * invb \
+                                        : 0.f;                                               \
+    float gv[CL];                                                                            \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) gv[c] = row_get(g, c);                    \
+    float2v gm2[NK / 2];                                                                     \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = float2v{0.f, 0.f};           \
+    _Pragma("unroll") for (int c = 0; c < CL; ++c) {                                         \
+      _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) gm2[j] = __builtin_elementwise_fma( \
+          float2v{gv[c], gv[c]},                                                             \
+          half2(c < SPL ? zr[R_][c < SPL ? c : 0][j >> 1] : zl[c < SPL ? 0 : c - SPL][j >> 1], j & 1), \
+          gm2[j]);                                                                           \
+    }                                                                                        \
+    float gme[NK];                                                                           \
+    _Pragma("unroll") for (int j = 0; j < NK / 2; ++j) {                                     \
+      gme[2 * j] = gm2[j].x;                                                                 \
+      gme[2 * j + 1] = gm2[j].y;                                                             \
+    }                                                                                        \
+    MR_STAMP(2)                                                                              \
+    labq[R_] = y[idxq[R_]];                                                                  \
+    QL_ISSUE(R_, idxq[R_]);                                                                  \
+    idxq[R_] = fetch_row();                                                                  \
+    MR_STAMP(6)                                                                              \
+    float t[NK / 2];                                                                         \
+    {                                                                                        \
+      float sa[NK / 2], sb[NK / 2];                                                          \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        sa[i] = gme[i];                                                                      \
+        sb[i] = gme[i + NK / 2];                                                             \
+      }                                                                                      \
+      swap_batch<32, NK / 2>(sa, sb);                                                        \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = sa[i] + sb[i];               \
+    }                                                                                        \
+    float u[KP];                                                                             \
+    {                                                                                        \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        sa[i] = t[i];                                                                        \
+        sb[i] = t[i + KP];                                                                   \
+      }                                                                                      \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = sa[i] + sb[i];                   \
+    }                                                                                        \
+    const int par = s & 1;                                                                   \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
+    MR_STAMP(3)                                                                              \
+    lds_barrier();                 /* B_s: also releases slot R_ to the loaders */          \
+    MR_STAMP(4)                                                                              \
+    _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                         \
+      float gs = gx[par][0][lane * KP + i];                                                  \
+      _Pragma("unroll") for (int k = 1; k < MQ_WAVES; ++k) gs += gx[par][k][lane * KP + i];  \
+      momentum_step_sel(po[i], bo[i], gs, first, mom, lr, n0 + kj0 + i < N);                 \
+    }                                                                                        \
+    first = 0;                                                                               \
+    {                                                                                        \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) sa[i] = sb[i] = po[i];                  \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        t[i] = sa[i];                                                                        \
+        t[i + KP] = sb[i];                                                                   \
+      }                                                                                      \
+      float ga[NK / 2], gb2[NK / 2];                                                         \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) ga[i] = gb2[i] = t[i];              \
+      swap_batch<32, NK / 2>(ga, gb2);                                                       \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        pr[i] = ga[i];                                                                       \
+        pr[i + NK / 2] = gb2[i];                                                             \
+      }                                                                                      \
+    }                                                                                        \
+    MR_STAMP(5)                                                                              \
+    ++s;                                                                                     \
+    if (pf_prog && (s & 3) == 0) mix_publish_progress(pf_prog, s);                           \
+  }
+  for (;;) {
+    QL_STEP(0)
+    QL_STEP(1)
+  }
+#undef QL_STEP
+#undef QL_ISSUE
+  if (pf_prog) mix_publish_progress(pf_prog, total);
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      const int n = n0 + kj0 + i;
+      if (n < N) {
+        p[n] = po[i];
+        buf[n] = bo[i];
+      }
+    }
+    if (lane == 0 && total > 0) *first_flag = 0;
+#ifdef FS_MIX_STAMPS
+    if (lane < 6) reinterpret_cast<unsigned long long*>(buf + N + 8)[lane] = mr_acc[lane];
+#endif
+  }
+}
+
 template <int NK, int CL, int SPL = quad_split<CL>()>
 static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C,
                             int nv, int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first,
@@ -1114,6 +1446,16 @@ static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, co
   // softmax on v_exp_f32 / v_rcp_f32 (e / sum) by default: config 2 1.28-1.29 -> 1.21-1.23 us per
   // step (r02s2fx), within the fp32 tolerance of the oracle like every other solver;
   // fs_tuning.mix_exact_softmax: torch's exp(o - m - log(sum)) form with libm expf / logf
+  // loader waves (mix_solve_quadl_kernel): config 2's instance (NK = 8, CL = 10) by default,
+  // fs_tuning.mix_quad_loaders = -1 off
+  if constexpr (NK == 8 && CL == 10 && SPL < CL) {
+    if (!tuning().mix_exact_softmax && tuning().mix_quad_loaders >= 0) {
+      hipLaunchKernelGGL((mix_solve_quadl_kernel<NK, CL, SPL>), dim3(blocks), dim3(2 * MQ_WAVES * 64), 0, st, Z, y,
+                         perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
+                         pf.lead);
+      return;
+    }
+  }
   if (!tuning().mix_exact_softmax)
     hipLaunchKernelGGL((mix_solve_quad_kernel<NK, CL, depth, SPL, true>), dim3(blocks), dim3(MQ_WAVES * 64), 0, st, Z,
                        y, perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
@@ -1938,10 +2280,26 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     QM_ISSUE(R_, idxq[R_], 0, SPL);                                                          \
     late_row = idxq[R_];                                                                     \
     idxq[R_] = fetch_row();                                                                  \
-    float t[NK / 2];                                                                         \
-    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = rs_level<32, true>(gme[i], gme[i + NK / 2], lane); \
+    float t[NK / 2];               /* = rs_level<32> / <16>, one pad per level */            \
+    {                                                                                        \
+      float sa[NK / 2], sb[NK / 2];                                                          \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        sa[i] = gme[i];                                                                      \
+        sb[i] = gme[i + NK / 2];                                                             \
+      }                                                                                      \
+      swap_batch<32, NK / 2>(sa, sb);                                                        \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) t[i] = sa[i] + sb[i];               \
+    }                                                                                        \
     float u[KP];                                                                             \
-    _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = rs_level<16, true>(t[i], t[i + KP], lane); \
+    {                                                                                        \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        sa[i] = t[i];                                                                        \
+        sb[i] = t[i + KP];                                                                   \
+      }                                                                                      \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) u[i] = sa[i] + sb[i];                   \
+    }                                                                                        \
     const int par = s & 1;                                                                   \
     _Pragma("unroll") for (int i = 0; i < KP; ++i) gx[par][w][lane * KP + i] = u[i];         \
     MR_STAMP(4)                                                                              \
@@ -1953,8 +2311,22 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
       momentum_step_sel(po[i], bo[i], gs, first, mom, lr, n0 + kj0 + i < N);                 \
     }                                                                                        \
     first = 0;                                                                               \
-    _Pragma("unroll") for (int i = 0; i < KP; ++i) gather_pair<16>(po[i], t[i], t[i + KP]);  \
-    _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) gather_pair<32>(t[i], pr[i], pr[i + NK / 2]); \
+    {                              /* = gather_pair<16> / <32>, one pad per level */         \
+      float sa[KP], sb[KP];                                                                  \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) sa[i] = sb[i] = po[i];                  \
+      swap_batch<16, KP>(sa, sb);                                                            \
+      _Pragma("unroll") for (int i = 0; i < KP; ++i) {                                       \
+        t[i] = sa[i];                                                                        \
+        t[i + KP] = sb[i];                                                                   \
+      }                                                                                      \
+      float ga[NK / 2], gb2[NK / 2];                                                         \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) ga[i] = gb2[i] = t[i];              \
+      swap_batch<32, NK / 2>(ga, gb2);                                                       \
+      _Pragma("unroll") for (int i = 0; i < NK / 2; ++i) {                                   \
+        pr[i] = ga[i];                                                                       \
+        pr[i + NK / 2] = gb2[i];                                                             \
+      }                                                                                      \
+    }                                                                                        \
     MR_STAMP(6)                                                                              \
     ++s;                                                                                     \
     if (pf_prog && k == 0) mix_publish_progress(pf_prog, s);   /* every step: helpers pace on it */ \

@@ -660,6 +660,42 @@ def test_mix_solve_prefetch_helpers(amd, N, C, nv, Bv, h, lead, solver):
         test_mix_solve_variants(amd, N, C, nv, Bv)
 
 
+@pytest.mark.parametrize('h', [-1, 4])
+@pytest.mark.parametrize('N,C,nv,Bv', [
+    (100, 10, 517, 16),     # config 2 shape: ragged last batch, lanes past ldN (column-0 reads, p = 0)
+    (128, 10, 77, 8),       # every lane's clients real, Bv = 8 (idle row groups)
+    (65, 9, 211, 16),       # C = 9 < CL = 10 (class padding in the LDS ring)
+    (97, 10, 16, 16),       # one batch per epoch: total = 3 steps (the loaders' tail)
+])
+def test_mix_solve_quad_loader_waves(amd, N, C, nv, Bv, h):
+    """The quarter-wave solver with loader waves (fs_tuning.mix_quad_loaders, default at config
+    2's instance: 4 waves stream the late classes' Z rows into a 2-slot LDS ring) is bitwise the
+    quarter-wave solver without them, with and without L2 helpers, and matches the oracle."""
+    rs = np.random.RandomState(N + nv + 7)
+    D = 64
+    Xv = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
+    yv = torch.from_numpy(rs.randint(0, C, size=nv).astype(np.int64))
+    p0 = torch.from_numpy(rs.dirichlet(np.ones(N)).astype(np.float32))
+    Ws = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.5).astype(np.float32))
+    dev = torch.device('cuda')
+    out = []
+    for loaders in (-1, 0):
+        with amd.lib.tuning(mix_solver='quad', mix_prefetch=h, mix_quad_loaders=loaders):
+            mix = amd.engine.Mixture(Xv, yv, D, C, N, Bv, p0, dev)
+            Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+            Wd[:, :, :D] = Ws
+            for rnd in range(2):
+                torch.manual_seed(70 + rnd)
+                mix.solve(Wd, amd.rng.draw_pass_seeds(3), 0.5)
+            torch.cuda.synchronize()
+            mix.check_errors()
+        assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'quad'
+        out.append((mix.p.cpu().clone(), mix.buf.cpu().clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    with amd.lib.tuning(mix_solver='quad', mix_prefetch=h):
+        test_mix_solve_variants(amd, N, C, nv, Bv)
+
+
 @pytest.mark.parametrize('solver,N,C', [('global', 100, 10), ('global', 300, 4), ('staged', 100, 10),
                                         ('mc', 1000, 7), ('reg', 100, 10), ('reg', 10, 2), ('wave', 10, 2),
                                         ('quad', 10, 2), ('reg2', 100, 10)])
