@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_quad_kernel(
 #define MQ_ISSUE(R_, ROW_, C0_, C1_)                                                         \
   {                                                                                          \
     const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
-    _Pragma("unroll") for (int c = C0_; c < C1_; ++c) {                                      \
+    _Pragma("unroll") for (int c = (C0_); c < (C1_); ++c) {                                      \
       _Pragma("unroll") for (int h = 0; h < NV4; ++h) zr[R_][c][h] = __builtin_bit_cast(     \
           floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[h], sofs[c], 0));   \
     }                                                                                        \
@@ -2173,7 +2173,7 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
 #define QM_ISSUE(R_, ROW_, C0_, C1_)                                                         \
   {                                                                                          \
     const uint32_t ro_ = (uint32_t)(ROW_) * (uint32_t)CN * 4u;                               \
-    _Pragma("unroll") for (int c = C0_; c < C1_; ++c) {                                      \
+    _Pragma("unroll") for (int c = (C0_); c < (C1_); ++c) {                                      \
       _Pragma("unroll") for (int h = 0; h < NV4; ++h) zr[R_][c][h] = __builtin_bit_cast(     \
           floatx4, __builtin_amdgcn_raw_buffer_load_b128(zrs, ro_ + lofs[h], sofs[c], 0));   \
     }                                                                                        \
