@@ -84,6 +84,8 @@ const char* fs_last_error(void);
  *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
  *                      of the K-partial sums (a different client-to-workgroup split)
+ *   split_teams        (ABI 13) fs_local_train_plan's choice of the team form for parallel
+ *                      clients: 0 = by shape, 1 = wherever it fits, -1 = never
  *   mix_quad_loaders   (ABI 13) quad p-solver at 64 < N <= 128, C <= 10 (config 2): 0 = with
  *                      4 loader waves that stream the late classes' Z rows into LDS (default),
  *                      -1 = without (each compute wave issues all of its loads); bitwise the
@@ -112,6 +114,7 @@ typedef struct fs_tuning {
   int split_early;
   int mix_qmc_lane_clients;
   int mix_quad_loaders;
+  int split_teams;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -191,13 +194,19 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              time interleaved, so one client's hand-off overlaps the other's compute and
  *              the feature rows stream through every phase; the same arithmetic as the split
  *              form at width G (bitwise the same results).
+ *              G | FS_G_TEAMS (ABI 13, parallel clients, G = 4 or 8): the "team" form --
+ *              min(ceil(N/2), CUs/G) groups of G workgroups, each workgroup's 8 waves two
+ *              teams of 4 that train two clients at once with team-local barriers, so one
+ *              team's hand-off and softmax run beside the other team's MFMAs (the split
+ *              arithmetic with 4 waves per slice: within the fp32 tolerance of the split form).
  *              fs_local_train_plan: *G_out on entry is a request (0 = planner's choice, 1 =
  *              one workgroup per client, 2..16 = that split width if the shape allows it,
- *              G | FS_G_PAIR = the pair form at that width if the shape allows it); prox says
- *              whether the FedProx term is on.
+ *              G | FS_G_PAIR = the pair form, G | FS_G_TEAMS = the team form at that width
+ *              if the shape allows it); prox says whether the FedProx term is on.
  * Requires 1 <= C <= 32, B <= 64, ld % 64 == 0, D <= ld.
  * ------------------------------------------------------------------------- */
 #define FS_G_PAIR 256
+#define FS_G_TEAMS 512
 int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                         int* G_out, int64_t* ws_bytes_out);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,

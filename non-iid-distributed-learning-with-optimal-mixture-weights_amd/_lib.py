@@ -71,6 +71,7 @@ ABI_VERSION = 13
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
+G_TEAMS = 512            # fs_local_train_plan: G | G_TEAMS = the team form at width G (ABI 13)
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
 SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc', 10: 'bin'}
 SOLVERS = {v: k for k, v in SOLVER_NAMES.items() if k}
@@ -82,7 +83,7 @@ class Tuning(C.Structure):
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
                 ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int),
-                ('mix_quad_loaders', C.c_int)]
+                ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int)]
 
 
 class PlanDesc(C.Structure):

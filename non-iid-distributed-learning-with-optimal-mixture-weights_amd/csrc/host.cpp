@@ -53,6 +53,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": mix_qmc_lane_clients must be 0, 4 or 8");
   if (t && (t->mix_quad_loaders < -1 || t->mix_quad_loaders > 0))
     return fail(FS_EINVAL, std::string(fn) + ": mix_quad_loaders must be -1 or 0");
+  if (t && (t->split_teams < -1 || t->split_teams > 1))
+    return fail(FS_EINVAL, std::string(fn) + ": split_teams must be -1, 0 or 1");
   return FS_OK;
 }
 

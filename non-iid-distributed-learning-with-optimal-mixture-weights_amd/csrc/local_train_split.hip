@@ -89,10 +89,18 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 // Round 3: odd groups started half a step late (so half the CUs stream while the other half
 // hand off) changed nothing (configs 2 / 4 / 5 within 0.5 %): the row stream is bound per CU,
 // not by the chip's HBM.
-template <int RT, int G, bool PROX, int EARLY>
+// TEAMS = 2 (round 4, the "team" form, G | FS_G_TEAMS): the workgroup's 8 waves are two teams
+// of 4 (one wave of each per SIMD), each training its own client lane with its own slice
+// image, hand-off slots and team-local barriers (an LDS arrival counter, not s_barrier), so
+// the two waves of a SIMD are in different phases: one team's hand-off, softmax and barriers
+// run beside the other team's MFMAs.  Per wave the work is the split form's at 4 waves per
+// slice (TPW = 2 tiles), so a team form at width G holds the registers of the split form at
+// width G / 2.
+template <int RT, int G, bool PROX, int EARLY, int TEAMS>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   static_assert(EARLY == 0 || !PROX, "early row issue: the prox anchor's loads would queue behind it");
-  constexpr int NW = SP_WAVES;
+  static_assert(TEAMS == 1 || TEAMS == 2, "teams");
+  constexpr int NW = SP_WAVES / TEAMS;             // waves per client lane
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
@@ -105,17 +113,27 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   // wave partial logits in the MFMA accumulator's own layout, [rt][lg][class][i] = row
   // 16 rt + 4 lg + i: one conflict-free ds_write_b128 per row tile, and the (row, class)
   // reads of the publish stride 4 words across a 16-lane row (conflict-free too)
-  __shared__ __attribute__((aligned(16))) float zpart[NW][NR * NC];
-  __shared__ float gbuf[NR][NC];
-  __shared__ float zsum[NR][NC];
-  __shared__ int lab[2][NR];
-  __shared__ float wred[NW][2];
-  __shared__ float wce[NW];
-  __shared__ float nrm[2];
-  extern __shared__ __attribute__((aligned(16))) float xs_lds[];   // [NR][RS] batch slice image
+  __shared__ __attribute__((aligned(16))) float zpart_t[TEAMS][NW][NR * NC];
+  __shared__ float gbuf_t[TEAMS][NR][NC];
+  __shared__ float zsum_t[TEAMS][NR][NC];
+  __shared__ int lab_t[TEAMS][2][NR];
+  __shared__ float wred_t[TEAMS][NW][2];
+  __shared__ float wce_t[TEAMS][NW];
+  __shared__ float nrm_t[TEAMS][2];
+  __shared__ unsigned tbar[TEAMS];                 // team barrier arrival counters
+  extern __shared__ __attribute__((aligned(16))) float xs_dyn[];   // TEAMS x [NR][RS] batch slice images
 
-  const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
+  // team-local thread and wave ids (the whole workgroup when TEAMS == 1)
+  const int team = __builtin_amdgcn_readfirstlane((int)threadIdx.x / NTH);
+  const int tid = (int)threadIdx.x - team * NTH, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform for the compiler
+  auto& zpart = zpart_t[team];
+  auto& gbuf = gbuf_t[team];
+  auto& zsum = zsum_t[team];
+  auto& lab = lab_t[team];
+  auto& wred = wred_t[team];
+  auto& wce = wce_t[team];
+  auto& nrm = nrm_t[team];
   const int64_t ld = P.ld;
   const int NT = (int)(ld >> 6);
   const int C = P.C, B = P.B, E = P.E;
@@ -130,7 +148,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   const int nb = gridDim.x - P.fuse_E;
   if ((int)blockIdx.x >= nb) {
     eval_persistent<SP_WAVES>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
-                         xs_lds, P.fuse_part);
+                         xs_dyn, P.fuse_part);
     return;
   }
   int lin;
@@ -141,15 +159,42 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
     lin = blockIdx.x;
     if (nb % 8 == 0) lin = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
   }
-  const int ng = X.ngroups;
-  const int grp = lin / G, g = lin % G;
-  if (grp >= ng) return;
+  const int ngp = X.ngroups;                     // groups of G workgroups
+  const int grpp = lin / G, g = lin % G;
+  if (grpp >= ngp) return;
+  // client lanes: TEAMS per group, each with its own client sequence and hand-off slots
+  const int ng = ngp * TEAMS, grp = grpp * TEAMS + team;
   const int T = P.chained ? P.N : (P.N + ng - 1) / ng;     // client sequence length
   const int t0 = tile_lo(g, G, NT), t1 = tile_lo(g + 1, G, NT);
   const int NTS = t1 - t0;                       // tiles of this slice
   const int RS = NTS * 64 + 8;                   // LDS row stride (floats)
+  float* const xs_lds = xs_dyn + team * (NR * RS);
   const float* start = P.W_start;
   unsigned long long* xb = X.xbuf + (int64_t)grp * 2 * G * X.SZ;
+  // barrier of this lane's waves: s_barrier for the whole workgroup, or (TEAMS == 2) an LDS
+  // arrival counter -- waits for this wave's LDS operations only (never for its row stream)
+  // (bounded like every spin: a timeout sets the error word and stops waiting)
+  unsigned tb_target = 0;
+  bool tb_dead = false;
+  if (TEAMS > 1 && tid == 0) tbar[team] = 0u;
+  auto team_sync = [&]() {
+    if constexpr (TEAMS == 1) {
+      lds_barrier();
+    } else {
+      tb_target += NW;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&tbar[team], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (unsigned sp = 0; !tb_dead &&
+                            __hip_atomic_load(&tbar[team], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < tb_target;) {
+        if (++sp > 64u * SP_SPIN_LIMIT) {
+          if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tb_dead = true;
+        }
+        __builtin_amdgcn_s_sleep(1);               // yield the SIMD to the other team's wave
+      }
+      asm volatile("" ::: "memory");
+    }
+  };
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---- weights (and prox anchor) of this slice into registers: the round-start model ----
@@ -327,7 +372,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       for (int rt = 0; rt < RT; ++rt)
         st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
       SP_STAMP(1)
-      lds_barrier();  // S1: wave partials, norm partials of the previous update; the image is free
+      team_sync();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
 
       {
@@ -435,7 +480,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #pragma unroll
         for (int f = 0; f < NE1; ++f) issue_row(f);
       SP_STAMP(5)
-      lds_barrier();  // S2: summed logits and norms, the image
+      team_sync();  // S2: summed logits and norms, the image
       if constexpr (NE > 0)
 #pragma unroll
         for (int f = NE1; f < NE2; ++f) issue_row(f);
@@ -467,7 +512,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       }
       cep = wave_sum_dpp(cep, lane);
       if (lane == 0) wce[w] = cep;
-      lds_barrier();  // S3: g, CE partials
+      team_sync();  // S3: g, CE partials
       if constexpr (NE > 0)
 #pragma unroll
         for (int f = NE2; f < NE; ++f) issue_row(f);
@@ -608,7 +653,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #undef SP_XLOAD
 #undef SP_IMG_WRITE
 #ifdef FS_STAMPS
-  if (tid == 0 && X.stamps) {
+  if (threadIdx.x == 0 && X.stamps) {
     for (int k = 0; k < 8; ++k) X.stamps[blockIdx.x * 16 + k] = stamp_acc[k];
     X.stamps[blockIdx.x * 16 + 15] = (unsigned long long)gs;
   }
@@ -637,41 +682,46 @@ int device_cus() {
   return g_cus;
 }
 
-static size_t split_dyn_lds(int RT, int NT, int G) {
+static size_t split_dyn_lds(int RT, int NT, int G, int teams = 1) {
   const int tiles = (NT + G - 1) / G;
-  return sizeof(float) * (size_t)(RT * 16) * (size_t)(tiles * 64 + 8);
+  return sizeof(float) * (size_t)teams * (size_t)(RT * 16) * (size_t)(tiles * 64 + 8);
 }
 
-static size_t split_static_lds(int RT, int NW) {
+static size_t split_static_lds(int RT, int NW, int teams = 1) {
   const int NR = RT * 16;
-  return (size_t)NW * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + NW * 3 * 4 + 8 + 64;
+  return (size_t)teams * ((size_t)NW * NR * 16 * 4 + 2 * (size_t)NR * 16 * 4 + 2 * NR * 4 + NW * 3 * 4 + 8) + 64 +
+         4 * teams;
 }
 
 static int split_rt(int B) { return B <= 16 ? 1 : 2; }
 
-// can G workgroups split one client of this shape?
-static bool split_fits(int C, int B, int NT, int G) {
+// can G workgroups split one client of this shape (teams = 2: two client lanes of 4 waves per
+// workgroup, parallel clients only)?
+static bool split_fits(int C, int B, int NT, int G, int teams = 1) {
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
   if (C > 16 || B > 32 || NT < G) return false;
   const int RT = split_rt(B);
+  const int nw = SP_WAVES / teams;
   const int tiles = (NT + G - 1) / G;
-  if ((tiles + SP_WAVES - 1) / SP_WAVES > SP_TPW) return false;
+  if ((tiles + nw - 1) / nw > SP_TPW) return false;
   if (G >= 8 && RT * 16 * C + 2 > 512) return false;   // exchanged values: at most 512
-  return split_dyn_lds(RT, NT, G) + split_static_lds(RT, SP_WAVES) <= 160 * 1024;
+  return split_dyn_lds(RT, NT, G, teams) + split_static_lds(RT, nw, teams) <= 160 * 1024;
 }
 
 static int split_sz(int RT) { return RT * 16 * 16 + 4; }
 
-// groups in flight: one per G workgroups, one workgroup per CU
-static int split_groups(int N, int G, int chained, int cus) {
-  return chained ? 1 : std::max(1, std::min(N, cus / G));
+// groups in flight: one per G workgroups, one workgroup per CU (each with `teams` client lanes)
+static int split_groups(int N, int G, int chained, int cus, int teams = 1) {
+  return chained ? 1 : std::max(1, std::min((N + teams - 1) / teams, cus / G));
 }
 
-static int64_t split_xbuf_bytes(int ngroups, int G, int RT) { return (int64_t)ngroups * 2 * G * split_sz(RT) * 8; }
+static int64_t split_xbuf_bytes(int ngroups, int G, int RT, int teams = 1) {
+  return (int64_t)ngroups * teams * 2 * G * split_sz(RT) * 8;
+}
 
-static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus) {
+static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus, int teams = 1) {
   const int RT = split_rt(B);
-  return split_xbuf_bytes(split_groups(N, G, chained, cus), G, RT) + SP_ERR_BYTES;
+  return split_xbuf_bytes(split_groups(N, G, chained, cus, teams), G, RT, teams) + SP_ERR_BYTES;
 }
 
 // the hand-off spin bound (fs_tuning.spin_limit); 0 = the injected-timeout test knob
@@ -681,12 +731,23 @@ static unsigned split_spin_limit() {
   return t.spin_limit ? t.spin_limit : SP_SPIN_LIMIT;
 }
 
-template <int RT, int G, bool PROX, int EARLY>
+template <int RT, int G, bool PROX, int EARLY, int TEAMS>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY, TEAMS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY>), dim3(grid), dim3(SP_THREADS), lds, st, P, X);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY, TEAMS>), dim3(grid), dim3(SP_THREADS), lds, st, P,
+                     X);
+}
+
+// the team form (G | FS_G_TEAMS): parallel clients, G = 4 or 8 (config 2 / 3 / 4 widths)
+template <int RT, int G>
+static void launch_split_teams(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  constexpr int EARLY_G = SP_EARLY;
+  const bool full = (P.ld >> 6) == (int64_t)G * (SP_WAVES / 2) * SP_TPW;
+  if (P.prox) launch_split_s<RT, G, true, 0, 2>(P, X, grid, lds, st);
+  else if (full && EARLY_G > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, EARLY_G, 2>(P, X, grid, lds, st);
+  else launch_split_s<RT, G, false, 0, 2>(P, X, grid, lds, st);
 }
 
 template <int RT, int G>
@@ -698,23 +759,27 @@ static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t
   // G = 16 6 (config 5: 5.34-5.36 vs 5.58 with 4)
   constexpr int EARLY_G = (G == 2 && SP_EARLY > 4) ? 4 : SP_EARLY;
   const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
-  if (P.prox) launch_split_s<RT, G, true, 0>(P, X, grid, lds, st);
-  else if (full && EARLY_G > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, EARLY_G>(P, X, grid, lds, st);
-  else launch_split_s<RT, G, false, 0>(P, X, grid, lds, st);
+  if (P.prox) launch_split_s<RT, G, true, 0, 1>(P, X, grid, lds, st);
+  else if (full && EARLY_G > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, EARLY_G, 1>(P, X, grid, lds, st);
+  else launch_split_s<RT, G, false, 0, 1>(P, X, grid, lds, st);
 }
 
-int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
+int launch_local_train_split(const LTParams& P, int Gf, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const int teams = (Gf & FS_G_TEAMS) ? 2 : 1;
+  const int G = Gf & (FS_G_PAIR - 1);
+  if (teams > 1 && (P.chained || !(G == 4 || G == 8)))
+    return fail(FS_EUNSUPPORTED, "fs_local_train: the team form runs parallel clients at G = 4 or 8");
   const int RT = split_rt(P.B);
   const int NT = (int)(P.ld >> 6);
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return fail(FS_EINVAL, "fs_local_train: G must be 1, 2, 4, 8 or 16");
   if (P.C > 16 || P.B > 32) return fail(FS_EUNSUPPORTED, "fs_local_train: split clients need C <= 16, B <= 32");
   if (NT < G) return fail(FS_EUNSUPPORTED, "fs_local_train: fewer feature tiles than workgroups per client");
-  if (!split_fits(P.C, P.B, NT, G)) return fail(FS_EUNSUPPORTED, "fs_local_train: slice too wide for one workgroup");
+  if (!split_fits(P.C, P.B, NT, G, teams)) return fail(FS_EUNSUPPORTED, "fs_local_train: slice too wide for one workgroup");
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
   if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");
-  const int ng = split_groups(P.N, G, P.chained, cus);
-  const int64_t xbytes = split_xbuf_bytes(ng, G, RT);
+  const int ng = split_groups(P.N, G, P.chained, cus, teams);
+  const int64_t xbytes = split_xbuf_bytes(ng, G, RT, teams);
   if (!ws || ws_bytes < xbytes + SP_ERR_BYTES) return fail(FS_EINVAL, "fs_local_train: workspace too small");
   char* base = reinterpret_cast<char*>(ws);
   SplitWS X;
@@ -734,7 +799,7 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
   // launch whose groups may run 2^20 - 1 steps or more (then the generation is 0: tags are
   // the step + 1 alone, as after any clearing).
   // (groups walk clients in snake order: at most ceil(N / ng) each; chained: all N)
-  const int64_t groups_clients = P.chained ? P.N : (P.N + ng - 1) / ng;
+  const int64_t groups_clients = P.chained ? P.N : (P.N + ng * teams - 1) / (ng * teams);
   const bool long_launch = P.max_client_steps <= 0 || P.max_client_steps * groups_clients >= (1 << 20) - 1;
   const unsigned gen = exchange_generation(ws, long_launch);
   X.tag_base = gen << 20;
@@ -742,10 +807,17 @@ int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_byte
     hipError_t e = hipMemsetAsync(base, 0, (size_t)xbytes, st);
     if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_local_train: ") + hipGetErrorString(e));
   }
-  const size_t lds = split_dyn_lds(RT, NT, G);
+  const size_t lds = split_dyn_lds(RT, NT, G, teams);
   if (P.fuse_E > 0 && (P.chained || ng * G + P.fuse_E > cus || lds < sizeof(float) * SP_WAVES * 16 * 17))
     return fail(FS_EINVAL, "fs_local_train: no room for the fused evaluation");
   const int grid = P.chained ? 8 * G : ng * G + P.fuse_E;
+  if (teams > 1) {
+    if (RT == 2 && G == 4) { launch_split_teams<2, 4>(P, X, grid, lds, st); return FS_OK; }
+    if (RT == 2 && G == 8) { launch_split_teams<2, 8>(P, X, grid, lds, st); return FS_OK; }
+    if (RT == 1 && G == 4) { launch_split_teams<1, 4>(P, X, grid, lds, st); return FS_OK; }
+    if (RT == 1 && G == 8) { launch_split_teams<1, 8>(P, X, grid, lds, st); return FS_OK; }
+    return fail(FS_EUNSUPPORTED, "fs_local_train: no team kernel for this shape");
+  }
 #define FS_SPLIT_CASE(rt, g) \
   if (RT == rt && G == g) { launch_split_g<rt, g>(P, X, grid, lds, st); return FS_OK; }
   FS_SPLIT_CASE(2, 2) FS_SPLIT_CASE(2, 4) FS_SPLIT_CASE(2, 8) FS_SPLIT_CASE(2, 16)
@@ -762,10 +834,12 @@ int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained) {
     if (chained || cus <= 0 || !pair_fits(C, B, NT, g)) return 0;
     return std::max(0, cus - pair_groups(N, g, cus) * g);
   }
-  if (chained || G < 2 || C > 16 || B > 32 || !split_fits(C, B, NT, G)) return 0;
+  const int teams = (G & FS_G_TEAMS) ? 2 : 1;
+  G &= FS_G_PAIR - 1;
+  if (chained || G < 2 || C > 16 || B > 32 || !split_fits(C, B, NT, G, teams)) return 0;
   const int cus = device_cus();
   if (cus <= 0) return 0;
-  return std::max(0, cus - split_groups(N, G, 0, cus) * G);
+  return std::max(0, cus - split_groups(N, G, 0, cus, teams) * G);
 }
 
 }  // namespace fs
@@ -789,6 +863,15 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   const int cus = device_cus();
   if (want == 1 || C > 16 || B > 32 || cus <= 0) return FS_OK;
   const int NT = (int)(ld >> 6);
+  // an explicit team request
+  if (want & FS_G_TEAMS) {
+    const int g = want & (FS_G_PAIR - 1);
+    if (!chained && (g == 4 || g == 8) && split_fits(C, B, NT, g, 2) && g <= cus) {
+      *G_out = g | FS_G_TEAMS;
+      *ws_bytes_out = split_ws_bytes(N, g, B, 0, cus, 2);
+      return FS_OK;
+    }
+  }
   // an explicit pair request
   if (want & FS_G_PAIR) {
     const int g = want & (FS_G_PAIR - 1);
@@ -799,6 +882,15 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
     }
   }
   int G = (want > 1 && want < FS_G_PAIR && split_fits(C, B, NT, want) && want <= cus) ? want : 0;
+  // the team form by tuning (fs_tuning.split_teams = 1: wherever it fits, at the narrowest
+  // width; 0 = by shape: not yet chosen automatically; -1 never)
+  if (G == 0 && !chained && tuning().split_teams > 0)
+    for (int cand : {4, 8})
+      if (split_fits(C, B, NT, cand, 2) && cand <= cus) {
+        *G_out = cand | FS_G_TEAMS;
+        *ws_bytes_out = split_ws_bytes(N, cand, B, 0, cus, 2);
+        return FS_OK;
+      }
   if (G == 0) {
     if (chained) {
       // one group walks the chain: slice one step's batch (B x ld floats) to ~32 KB per CU

@@ -136,7 +136,8 @@ class LocalTrainer:
     workgroups splits each client's feature dimension whenever the shape allows, in parallel
     mode as persistent groups over the clients -- two clients per group in the pair form
     (G | _lib.G_PAIR) where the shape allows it -- in chained mode as one group walking the
-    chain); 1 forces one workgroup per client, G a split width, G | _lib.G_PAIR the pair form."""
+    chain); 1 forces one workgroup per client, G a split width, G | _lib.G_PAIR the pair form,
+    G | _lib.G_TEAMS the team form."""
 
     def __init__(self, feats, C, B, E, split=None, chained=False, rows=None, prox=False):
         self.f = feats
@@ -168,6 +169,7 @@ class LocalTrainer:
                                    % (int(split), g.value))
         self.G = int(g.value)                       # as the ABI takes it (G | G_PAIR: the pair form)
         self.pair = bool(self.G & _lib.G_PAIR)
+        self.teams = bool(self.G & _lib.G_TEAMS)
         self.width = self.G & (_lib.G_PAIR - 1)     # workgroups per client group
         self.ws = (torch.zeros(max(2 * _lib.ERR_BLOCK, int(wsb.value)), dtype=torch.uint8, device=dev)
                    if self.G > 1 else None)
@@ -178,7 +180,7 @@ class LocalTrainer:
             return 1 if self.chained else self.N
         if self.chained:
             return 1
-        per = (self.N + 1) // 2 if self.pair else self.N
+        per = (self.N + 1) // 2 if (self.pair or self.teams) else self.N
         return max(1, min(per, cus // self.width))
 
     @property

@@ -28,6 +28,7 @@ def main():
     ap.add_argument('--G', type=int, default=0)
     ap.add_argument('--chained', action='store_true')
     ap.add_argument('--pair', action='store_true', help='the pair form at width --G (or the planner\'s)')
+    ap.add_argument('--teams', action='store_true', help='the team form at width --G (team 0 stamped)')
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
     sh = SHAPES[a.config]
@@ -36,7 +37,7 @@ def main():
     N, D, C, E, B = sh['clients'], sh['D'], sh['C'], 2, 32
     d = data.federated(N, sh['rows'], D, C, 1000, shape=sh['shape'], device=dev)
     feats = engine.Features(d['X_train'], d['y_train'], D, dev)
-    split = (a.G | fedamw_amd._lib.G_PAIR if a.pair else a.G) or None
+    split = (a.G | fedamw_amd._lib.G_PAIR if a.pair else (a.G | fedamw_amd._lib.G_TEAMS if a.teams else a.G)) or None
     tr = engine.LocalTrainer(feats, C, B, E, split=split, chained=chained)
     names = PAIR_NAMES if tr.pair else NAMES
     cus = torch.cuda.get_device_properties(0).multi_processor_count

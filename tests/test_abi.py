@@ -103,5 +103,8 @@ def test_tuning_threading_contract():
         bad = _lib.Tuning(mix_quad_loaders=1)
         assert L.fs_set_thread_tuning(ctypes.byref(bad)) == -1
         assert 'mix_quad_loaders' in L.fs_last_error().decode()
+        bad = _lib.Tuning(split_teams=2)
+        assert L.fs_set_thread_tuning(ctypes.byref(bad)) == -1
+        assert 'split_teams' in L.fs_last_error().decode()
     finally:
         _lib.set_tuning(**prev)
