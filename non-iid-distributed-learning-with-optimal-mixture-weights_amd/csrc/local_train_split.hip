@@ -124,7 +124,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   extern __shared__ __attribute__((aligned(16))) float xs_dyn[];   // TEAMS x [NR][RS] batch slice images
 
   // team-local thread and wave ids (the whole workgroup when TEAMS == 1)
-  const int team = __builtin_amdgcn_readfirstlane((int)threadIdx.x / NTH);
+  // (a compile-time 0 for TEAMS == 1: the split form's addressing stays exactly round 3's)
+  const int team = TEAMS > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / NTH) : 0;
   const int tid = (int)threadIdx.x - team * NTH, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform for the compiler
   auto& zpart = zpart_t[team];
@@ -168,7 +169,12 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   const int t0 = tile_lo(g, G, NT), t1 = tile_lo(g + 1, G, NT);
   const int NTS = t1 - t0;                       // tiles of this slice
   const int RS = NTS * 64 + 8;                   // LDS row stride (floats)
-  float* const xs_lds = xs_dyn + team * (NR * RS);
+  // this lane's slice image; an expression, not a pointer variable: through a local pointer
+  // hipcc lost the image's distinctness from the static LDS arrays and waited lgkmcnt(0) in
+  // three places of the step (config 5: 5.28 -> 6.09 ms per launch, profiles/r04/teams_split_regression.txt);
+  // so the split form (TEAMS == 1) compiles to exactly round 3's code
+  const int xs_off = TEAMS > 1 ? team * (NR * RS) : 0;
+#define xs_lds (xs_dyn + xs_off)
   const float* start = P.W_start;
   unsigned long long* xb = X.xbuf + (int64_t)grp * 2 * G * X.SZ;
   // barrier of this lane's waves: s_barrier for the whole workgroup, or (TEAMS == 2) an LDS
@@ -652,6 +658,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   }
 #undef SP_XLOAD
 #undef SP_IMG_WRITE
+#undef xs_lds
 #ifdef FS_STAMPS
   if (threadIdx.x == 0 && X.stamps) {
     for (int k = 0; k < 8; ++k) X.stamps[blockIdx.x * 16 + k] = stamp_acc[k];
