@@ -1448,9 +1448,11 @@ static void launch_mix_quad(hipStream_t st, const float* Z, const int32_t* y, co
   // fs_tuning.mix_exact_softmax: torch's exp(o - m - log(sum)) form with libm expf / logf
   // loader waves (mix_solve_quadl_kernel): config 2's instance (NK = 8, CL = 10) by default,
   // fs_tuning.mix_quad_loaders = -1 off
+  // (2 classes in the register ring, 8 through the LDS ring: 0.837-0.839 us per step against
+  // 0.851-0.856 with 3 and 0.851-0.874 with 1, profiles/r04/quad_loader_split.txt)
   if constexpr (NK == 8 && CL == 10 && SPL < CL) {
     if (!tuning().mix_exact_softmax && tuning().mix_quad_loaders >= 0) {
-      hipLaunchKernelGGL((mix_solve_quadl_kernel<NK, CL, SPL>), dim3(blocks), dim3(2 * MQ_WAVES * 64), 0, st, Z, y,
+      hipLaunchKernelGGL((mix_solve_quadl_kernel<NK, CL, 2>), dim3(blocks), dim3(2 * MQ_WAVES * 64), 0, st, Z, y,
                          perms, N, C, nv, epochs, Bv, lr, mom, p, buf, first, z_bytes, pf.prog, std::min(pf.h, 31),
                          pf.lead);
       return;
