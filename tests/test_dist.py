@@ -129,6 +129,52 @@ def test_two_rank_sharded_z_layout():
     np.testing.assert_array_equal(ps[pos], p)
 
 
+def _zb_worker(rank, world, port, out):
+    """Blocked all-gather (the sharded FedAMW path at every world size the driver runs):
+    out's storage holds [R][n_v][C][L], rank r's block its clients in shard order."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    tdist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        rs = np.random.RandomState(7)
+        N, C, nv = 37, 4, 6
+        ns = rs.randint(10, 100, size=N)
+        Zg = rs.normal(size=(nv, C, N)).astype(np.float32)
+        shards = dist.shard_lpt(dist.client_work(ns, 2, 32), world)
+        L, pos = dist.solver_layout(shards)
+        mine = shards[rank]
+        Zl = np.zeros((nv, C, L), np.float32)
+        Zl[:, :, :len(mine)] = Zg[:, :, mine]
+        out_t = torch.empty(nv, C * world * L)
+        dist.allgather_z(torch.from_numpy(Zl.reshape(nv, C * L)), C, out_t, blocked=True)
+        out[rank] = (out_t.numpy(), L, pos)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_four_rank_blocked_z_layout():
+    """SURVEY 8(e), rehearsed at 4 ranks: the blocked all-gather leaves rank r's block at
+    [r][n_v][C][L] (no layout copy), client j at block pos[j] // L, column pos[j] % L, padding
+    columns zero -- the layout fs_mix_solve_blocked reads -- identically on every rank."""
+    world = 4
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_zb_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rs = np.random.RandomState(7)
+    N, C, nv = 37, 4, 6
+    rs.randint(10, 100, size=N)
+    Zg = rs.normal(size=(nv, C, N)).astype(np.float32)
+    Z0, L, pos = out[0]
+    for r in range(1, world):
+        np.testing.assert_array_equal(Z0, out[r][0])
+    Zb = Z0.reshape(world, nv, C, L)
+    for j in range(N):
+        np.testing.assert_array_equal(Zb[pos[j] // L, :, :, pos[j] % L], Zg[:, :, j])
+    used = np.zeros(world * L, bool)
+    used[pos] = True
+    assert (Zb.transpose(1, 2, 0, 3).reshape(nv, C, world * L)[:, :, ~used] == 0).all() and L % 4 == 0
+
+
 def _rank_check_worker(rank, world, port, out):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
