@@ -84,6 +84,8 @@ const char* fs_last_error(void);
  *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
  *                      of the K-partial sums (a different client-to-workgroup split)
+ *   mix_poll_delay     (ABI 13) qmc p-solver: s_sleep(1) units (~64 cycles each) between a
+ *                      step's publish and its first poll: 0 = by shape, -1 = none, n > 0 = n
  *   split_teams        (ABI 13) fs_local_train_plan's choice of the team form for parallel
  *                      clients: 0 = by shape, 1 = wherever it fits, -1 = never
  *   mix_quad_loaders   (ABI 13) quad p-solver at 64 < N <= 128, C <= 10 (config 2): 0 = with
@@ -115,6 +117,7 @@ typedef struct fs_tuning {
   int mix_qmc_lane_clients;
   int mix_quad_loaders;
   int split_teams;
+  int mix_poll_delay;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);

@@ -83,7 +83,8 @@ class Tuning(C.Structure):
                 ('mix_exact_softmax', C.c_int), ('no_eval_fuse', C.c_int), ('spin_limit', C.c_uint),
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
                 ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int),
-                ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int)]
+                ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int),
+                ('mix_poll_delay', C.c_int)]
 
 
 class PlanDesc(C.Structure):

@@ -2105,7 +2105,8 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
     const float* __restrict__ Z, const int32_t* __restrict__ y, const int32_t* __restrict__ perms, int N, int C,
     int nv, int epochs, int Bv, float lr, float mom, float* __restrict__ p, float* __restrict__ buf,
     int* __restrict__ first_flag, int z_bytes, unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err,
-    int K, unsigned spin_limit, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead, int zL, int zR) {
+    int K, unsigned spin_limit, unsigned* __restrict__ pf_prog, int pf_h, int pf_lead, int zL, int zR,
+    int poll_delay) {
   static_assert(NK == 4 || NK == 8, "clients per lane");
   static_assert(CL >= 1 && CL <= 16, "classes");
   static_assert(DEPTH * (CL * NK / 4 + 2) <= 63, "ring vs the vmcnt window");
@@ -2230,6 +2231,10 @@ __global__ __launch_bounds__(MQ_WAVES * 64) void mix_solve_qmc_kernel(
                          ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(opart), \
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                        \
       unsigned long long gr[QMC_KMAX];                                                       \
+      /* wait ~64 poll_delay cycles before the first poll: the partners publish about then, \
+         and the polls of 16 workgroups x 4 waves on the same lines clog the L2 while they \
+         are early (profiles/r04/qmc_poll_delay_sweep.txt) */                                \
+      for (int d_ = 0; d_ < poll_delay; ++d_) __builtin_amdgcn_s_sleep(1);                   \
       _Pragma("unroll") for (int kk = 0; kk < QMC_KMAX; ++kk)                                \
         if (kk < K) gr[kk] = __hip_atomic_load(slot + (int64_t)kk * MC_SLOT + gi, __ATOMIC_RELAXED, \
                                                __HIP_MEMORY_SCOPE_AGENT);                    \
@@ -2370,6 +2375,17 @@ static int qmc_nk(int N, int C) {
   return (mix_ldn(N) + 63) / 64 <= QMC_KMAX ? 4 : 8;
 }
 
+// s_sleep(1) units before a step's first poll (fs_tuning.mix_poll_delay: 0 = by shape, -1 =
+// none, n > 0 = n).  By shape from the sweeps (profiles/r04/qmc_poll_delay*.txt, us per step,
+// none / best): N = 1000, C = 10 (K = 16) 3.24 / 2.73 at 14 (12-16 within 1 %); N = 1000, C = 4
+// 2.86 / 2.28 at 8 (2.49 at 16); N = 300 2.41 / 1.95 at 8; N = 520 2.68 / 2.07 at 8
+static int qmc_poll_delay(int K, int C) {
+  const int t = tuning().mix_poll_delay;
+  if (t < 0) return 0;
+  if (t > 0) return t;
+  return (K >= 12 && C >= 8) ? 14 : 8;
+}
+
 static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
   const int64_t zb = (int64_t)nv * C * mix_ldn(N) * 4;
   const int nk = qmc_nk(N, C);
@@ -2396,15 +2412,19 @@ static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const
   const int h = pf.prog ? std::min(pf.h, 32 - K) : 0;   // the solvers' XCD has 32 CUs
   const dim3 grid(MC_XCDS * (K + h)), block(MQ_WAVES * 64);
   const int zb = (int)((int64_t)nv * C * mix_ldn(N) * 4);
+  const int pd = qmc_poll_delay(K, C);
   if (nk == 8)
     hipLaunchKernelGGL((mix_solve_qmc_kernel<8, 10, 2, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR,
+                       pd);
   else if (C <= 10)
     hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 10, 3, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR,
+                       pd);
   else
     hipLaunchKernelGGL((mix_solve_qmc_kernel<4, 16, 2, quad_split<16>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
-                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR);
+                       epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR,
+                       pd);
   return 0;
 }
 

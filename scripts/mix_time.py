@@ -1,5 +1,5 @@
 """Diagnostic: fs_mix_solve time per dependent p-SGD step (and fs_mix_z) at a given shape.
-    [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] [FS_MIX_PF_H=h] [FS_MIX_PF_LEAD=l] [FS_MIX_QMC_LC=4|8] [FS_MIX_QUAD_LOADERS=-1]
+    [FS_MIX_SOLVER=name] [FS_MIX_EXACT=1] [FS_MIX_PF_H=h] [FS_MIX_PF_LEAD=l] [FS_MIX_QMC_LC=4|8] [FS_MIX_QUAD_LOADERS=-1] [FS_MIX_POLL_DELAY=n]
     [FS_MIX_DUMP=file.npy (p and buf after the run, for bitwise A/B of two builds)] python scripts/mix_time.py
         [N] [C] [n_val] [epochs] [D]
 (GPU box; default config 2; the variables only select fs_tuning fields for this run)"""
@@ -18,7 +18,8 @@ fedamw_amd._lib.set_tuning(mix_solver=SOLVER, mix_exact_softmax=int(os.environ.g
                            mix_prefetch=int(os.environ.get('FS_MIX_PF_H', '0')),
                            mix_prefetch_lead=int(os.environ.get('FS_MIX_PF_LEAD', '0')),
                            mix_qmc_lane_clients=int(os.environ.get('FS_MIX_QMC_LC', '0')),
-                           mix_quad_loaders=int(os.environ.get('FS_MIX_QUAD_LOADERS', '0')))
+                           mix_quad_loaders=int(os.environ.get('FS_MIX_QUAD_LOADERS', '0')),
+                           mix_poll_delay=int(os.environ.get('FS_MIX_POLL_DELAY', '0')))
 a = [int(x) for x in sys.argv[1:]]
 N, C, nv, ep, D = (a + [100, 10, 12800, 10, 2048][len(a):])[:5]
 dev = torch.device('cuda')

@@ -106,5 +106,8 @@ def test_tuning_threading_contract():
         bad = _lib.Tuning(split_teams=2)
         assert L.fs_set_thread_tuning(ctypes.byref(bad)) == -1
         assert 'split_teams' in L.fs_last_error().decode()
+        bad = _lib.Tuning(mix_poll_delay=-2)
+        assert L.fs_set_thread_tuning(ctypes.byref(bad)) == -1
+        assert 'mix_poll_delay' in L.fs_last_error().decode()
     finally:
         _lib.set_tuning(**prev)

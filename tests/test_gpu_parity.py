@@ -567,6 +567,34 @@ def test_mix_solve_qmc(amd, N, C, nv, Bv, h, lc):
     assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
 
 
+@pytest.mark.parametrize('N,C,nv', [(1000, 10, 97), (300, 4, 60)])
+def test_mix_solve_qmc_poll_delay_bitwise(amd, N, C, nv):
+    """The first-poll delay (fs_tuning.mix_poll_delay: none, by shape, a long one) changes only
+    when the polls go out: p and the momentum buffer are bitwise the same."""
+    rs = np.random.RandomState(N + 3)
+    D = 64
+    Xv = torch.from_numpy((np.cos(rs.normal(size=(nv, D))) / np.sqrt(D)).astype(np.float32))
+    yv = torch.from_numpy(rs.randint(0, C, size=nv).astype(np.int64))
+    p0 = torch.from_numpy(rs.dirichlet(np.ones(N)).astype(np.float32))
+    Ws = torch.from_numpy((rs.normal(size=(N, C, D)) * 0.5).astype(np.float32))
+    dev = torch.device('cuda')
+    out = []
+    for delay in (-1, 0, 40):
+        with amd.lib.tuning(mix_solver='qmc', mix_poll_delay=delay):
+            mix = amd.engine.Mixture(Xv, yv, D, C, N, 16, p0, dev)
+            Wd = torch.zeros(N, C, mix.f.ld, device=dev)
+            Wd[:, :, :D] = Ws
+            for rnd in range(2):
+                torch.manual_seed(30 + rnd)
+                mix.solve(Wd, amd.rng.draw_pass_seeds(3), 0.05)
+            torch.cuda.synchronize()
+            mix.check_errors()
+        assert amd.lib.SOLVER_NAMES[amd.lib.lib().fs_mix_solve_last_mode()] == 'qmc'
+        out.append((mix.p.cpu().clone(), mix.buf.cpu().clone()))
+    for o in out[1:]:
+        assert torch.equal(out[0][0], o[0]) and torch.equal(out[0][1], o[1])
+
+
 def test_mix_solve_qmc_timeout_raises(amd):
     """A timed-out exchange of the multi-CU quarter-wave solver sets the error word; the next
     solve is clean."""
