@@ -86,6 +86,8 @@ const char* fs_last_error(void);
  *                      of the K-partial sums (a different client-to-workgroup split)
  *   mix_poll_delay     (ABI 13) qmc p-solver: s_sleep(1) units (~64 cycles each) between a
  *                      step's publish and its first poll: 0 = by shape, -1 = none, n > 0 = n
+ *   split_poll_delay   (ABI 13) split form: s_sleep(1) units between a step's publish and its
+ *                      first poll: 0 = by width, -1 = none, n > 0 = n
  *   split_teams        (ABI 13) fs_local_train_plan's choice of the team form for parallel
  *                      clients: 0 = by shape, 1 = wherever it fits, -1 = never
  *   mix_quad_loaders   (ABI 13) quad p-solver at 64 < N <= 128, C <= 10 (config 2): 0 = with
@@ -118,6 +120,7 @@ typedef struct fs_tuning {
   int mix_quad_loaders;
   int split_teams;
   int mix_poll_delay;
+  int split_poll_delay;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);

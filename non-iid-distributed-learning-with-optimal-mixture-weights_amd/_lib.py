@@ -84,7 +84,7 @@ class Tuning(C.Structure):
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
                 ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int),
                 ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int),
-                ('mix_poll_delay', C.c_int)]
+                ('mix_poll_delay', C.c_int), ('split_poll_delay', C.c_int)]
 
 
 class PlanDesc(C.Structure):

@@ -57,6 +57,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": split_teams must be -1, 0 or 1");
   if (t && (t->mix_poll_delay < -1 || t->mix_poll_delay > 4096))
     return fail(FS_EINVAL, std::string(fn) + ": mix_poll_delay must be in [-1, 4096]");
+  if (t && (t->split_poll_delay < -1 || t->split_poll_delay > 4096))
+    return fail(FS_EINVAL, std::string(fn) + ": split_poll_delay must be in [-1, 4096]");
   return FS_OK;
 }
 

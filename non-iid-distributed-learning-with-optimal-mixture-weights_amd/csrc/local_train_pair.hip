@@ -632,6 +632,7 @@ int launch_local_train_pair(const LTParams& P, int G, void* ws, int64_t ws_bytes
     const fs_tuning t = tuning();
     X.spin_limit = t.inject_timeout ? 0u : (t.spin_limit ? t.spin_limit : PR_SPIN_LIMIT);
   }
+  X.poll_delay = 0;                    // (the pair form polls half a step after publishing)
   X.stamps = nullptr;
 #ifdef FS_STAMPS
   X.stamps = reinterpret_cast<unsigned long long*>(base + xbytes);

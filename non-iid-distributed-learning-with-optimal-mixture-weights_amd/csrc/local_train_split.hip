@@ -429,6 +429,10 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           };
+          // (wait before the first poll: partners publish about then, and early round trips of
+          // every wave on the same lines only clog the L2 -- as in the qmc p-solver)
+          if (h0 == 0)
+            for (int d_ = 0; d_ < X.poll_delay; ++d_) __builtin_amdgcn_s_sleep(1);
           poll();
           if (h0 == 0) SP_IMG_WRITE();
           for (;;) {
@@ -731,6 +735,18 @@ static int64_t split_ws_bytes(int N, int G, int B, int chained, int cus, int tea
   return split_xbuf_bytes(split_groups(N, G, chained, cus, teams), G, RT, teams) + SP_ERR_BYTES;
 }
 
+// s_sleep(1) units before a step's first poll (fs_tuning.split_poll_delay: 0 = by width, -1 =
+// none, n > 0 = n).  By width (profiles/r04/split_poll_delay_*.txt, launch ms): G = 16 (config 5)
+// 5.35-5.37 without, 5.21-5.23 at 16, 5.29-5.31 at 24, 5.45-5.49 at 48; G = 2 (config 2) no gain
+constexpr int SPLIT_PD_WIDE = 16, SPLIT_PD_NARROW = 0;
+static int split_poll_delay(int G, bool chained) {
+  const int t = tuning().split_poll_delay;
+  if (t < 0) return 0;
+  if (t > 0) return t;
+  if (chained) return 0;                 // one group: no other group's polls to yield to
+  return G >= 8 ? SPLIT_PD_WIDE : SPLIT_PD_NARROW;
+}
+
 // the hand-off spin bound (fs_tuning.spin_limit); 0 = the injected-timeout test knob
 static unsigned split_spin_limit() {
   const fs_tuning t = tuning();
@@ -795,6 +811,7 @@ int launch_local_train_split(const LTParams& P, int Gf, void* ws, int64_t ws_byt
   X.SZ = split_sz(RT);
   X.ngroups = ng;
   X.spin_limit = split_spin_limit();
+  X.poll_delay = split_poll_delay(G, P.chained != 0);
   X.stamps = nullptr;
 #ifdef FS_STAMPS
   X.stamps = reinterpret_cast<unsigned long long*>(base + xbytes);

@@ -29,6 +29,7 @@ struct SplitWS {
   unsigned tag_base;                   // launch generation << 20 (0: the buffer was zeroed for this launch)
   int ngroups;
   unsigned spin_limit;                 // 0: test knob -- report a timeout at the first hand-off
+  int poll_delay;                      // s_sleep(1) units between a step's publish and first poll
 };
 
 __device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
