@@ -84,16 +84,19 @@ const char* fs_last_error(void);
  *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
  *                      of the K-partial sums (a different client-to-workgroup split)
- *   mix_poll_delay     (ABI 13) qmc p-solver: s_sleep(1) units (~64 cycles each) between a
- *                      step's publish and its first poll: 0 = by shape, -1 = none, n > 0 = n
- *   split_poll_delay   (ABI 13) split form: s_sleep(1) units between a step's publish and its
- *                      first poll: 0 = by width, -1 = none, n > 0 = n
- *   split_teams        (ABI 13) fs_local_train_plan's choice of the team form for parallel
- *                      clients: 0 = by shape, 1 = wherever it fits, -1 = never
  *   mix_quad_loaders   (ABI 13) quad p-solver at 64 < N <= 128, C <= 10 (config 2): 0 = with
  *                      4 loader waves that stream the late classes' Z rows into LDS (default),
  *                      -1 = without (each compute wave issues all of its loads); bitwise the
  *                      same p
+ *   split_teams        (ABI 13) fs_local_train_plan's choice of the team form for parallel
+ *                      clients: 0 = by shape (not chosen: measured slower), 1 = wherever it
+ *                      fits, -1 = never
+ *   mix_poll_delay     (ABI 13) qmc p-solver: s_sleep(1) units (~64 cycles each) between a
+ *                      step's publish and its first poll: 0 = by shape (14 at K >= 12 with
+ *                      C >= 8, else 8), -1 = none, n > 0 = n; bitwise the same p
+ *   split_poll_delay   (ABI 13) split form: s_sleep(1) units between a step's publish and its
+ *                      first poll: 0 = by width (16 at G >= 8 with parallel clients, else
+ *                      none), -1 = none, n > 0 = n; bitwise the same results
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
