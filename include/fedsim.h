@@ -64,7 +64,7 @@ const char* fs_last_error(void);
  *   mix_prefetch       L2 prefetch helper workgroups beside the p-solve: 0 = by solver
  *                      (4 for the quarter-wave solver when Z outgrows the L2s, 24 for qmc),
  *                      -1 = none, n > 0 = n
- *   mix_prefetch_lead  steps the helpers run ahead (0 = by solver: 16 quad, 6 qmc)
+ *   mix_prefetch_lead  steps the helpers run ahead (0 = by solver: 16 quad, 8 qmc)
  *   mix_exact_softmax  quarter-wave solvers: 1 = torch's exp(o - m - log sum) form with libm
  *                      expf / logf (default: e * rcp(sum e) on v_exp_f32 / v_rcp_f32; both
  *                      within the fp32 tolerance of the reference)

@@ -2456,11 +2456,14 @@ static int mix_prefetch_setup(const fs_tuning& tune, bool use_quad, bool use_qmc
   const bool z_big = (int64_t)n_val * C * mix_ldn(N) * 4 > ((int64_t)16 << 20);
   const int h = tune.mix_prefetch > 0 ? tune.mix_prefetch
                 : (tune.mix_prefetch < 0 ? 0 : ((use_quad && z_big) ? 4 : (use_qmc ? 24 : 0)));
-  // default lead: 16 steps for the quarter-wave solver; 6 for qmc, whose helpers (round 4:
-  // LDS-DMA pieces, the solver's progress published every step) keep 6 x 640 KB of rows in
-  // the XCD's 4 MB L2 ahead of the solver at config 5 -- 24 helpers, leads 4 / 6 / 8 / 12:
-  // 3.85 / 3.62 / 3.76 / 3.81 us per step, none: 4.40 (profiles/r04/mix_solve_helper_sweep.txt)
-  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : (use_qmc ? 6 : 16);
+  // default lead: 16 steps for the quarter-wave solver; 8 for qmc, whose helpers (round 4:
+  // LDS-DMA pieces, the solver's progress published every step) keep a few steps of rows in
+  // the XCD's 4 MB L2 ahead of the solver -- at config 5 before the first-poll delay, 24
+  // helpers, leads 4 / 6 / 8 / 12: 3.85 / 3.62 / 3.76 / 3.81 us per step, none: 4.40
+  // (profiles/r04/mix_solve_helper_sweep.txt); with it (16 helpers at K = 16), leads 6 / 8 / 10
+  // / 12 / 16: 2.70-2.72 / 2.58 / 2.62-2.63 / 2.65 / 2.66, and at N = 300 1.96 for 6 and 8
+  // (profiles/r04/qmc_lead_sweep.txt)
+  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : (use_qmc ? 8 : 16);
   if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
     pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
     pf.h = h;
