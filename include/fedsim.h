@@ -64,7 +64,8 @@ const char* fs_last_error(void);
  *   mix_prefetch       L2 prefetch helper workgroups beside the p-solve: 0 = by solver
  *                      (4 for the quarter-wave solver when Z outgrows the L2s, 24 for qmc),
  *                      -1 = none, n > 0 = n
- *   mix_prefetch_lead  steps the helpers run ahead (0 = by solver: 16 quad, 8 qmc)
+ *   mix_prefetch_lead  steps the helpers run ahead (0 = by solver: 16 quad; qmc 8 at K >= 12
+ *                      workgroups, else 6)
  *   mix_exact_softmax  quarter-wave solvers: 1 = torch's exp(o - m - log sum) form with libm
  *                      expf / logf (default: e * rcp(sum e) on v_exp_f32 / v_rcp_f32; both
  *                      within the fp32 tolerance of the reference)
@@ -92,7 +93,7 @@ const char* fs_last_error(void);
  *                      clients: 0 = by shape (not chosen: measured slower), 1 = wherever it
  *                      fits, -1 = never
  *   mix_poll_delay     (ABI 13) qmc p-solver: s_sleep(1) units (~64 cycles each) between a
- *                      step's publish and its first poll: 0 = by shape (14 at K >= 12 with
+ *                      step's publish and its first poll: 0 = by shape (10 at K >= 12 with
  *                      C >= 8, else 8), -1 = none, n > 0 = n; bitwise the same p
  *   split_poll_delay   (ABI 13) split form: s_sleep(1) units between a step's publish and its
  *                      first poll: 0 = by width (16 at G >= 8 with parallel clients, else

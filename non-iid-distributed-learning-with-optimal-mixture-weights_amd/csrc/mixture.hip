@@ -2377,13 +2377,15 @@ static int qmc_nk(int N, int C) {
 
 // s_sleep(1) units before a step's first poll (fs_tuning.mix_poll_delay: 0 = by shape, -1 =
 // none, n > 0 = n).  By shape from the sweeps (profiles/r04/qmc_poll_delay*.txt, us per step,
-// none / best): N = 1000, C = 10 (K = 16) 3.24 / 2.73 at 14 (12-16 within 1 %); N = 1000, C = 4
-// 2.86 / 2.28 at 8 (2.49 at 16); N = 300 2.41 / 1.95 at 8; N = 520 2.68 / 2.07 at 8
+// none / best, at helper lead 6): N = 1000, C = 10 (K = 16) 3.24 / 2.73 at 14 (12-16 within 1 %);
+// N = 1000, C = 4 2.86 / 2.28 at 8 (2.49 at 16); N = 300 2.41 / 1.95 at 8; N = 520 2.68 / 2.07 at 8.
+// At lead 8 (the qmc default since) the K = 16 optimum moved to 10: 2.48 vs 2.58 us at 14
+// (profiles/r04/qmc_delay_lead_grid.txt).
 static int qmc_poll_delay(int K, int C) {
   const int t = tuning().mix_poll_delay;
   if (t < 0) return 0;
   if (t > 0) return t;
-  return (K >= 12 && C >= 8) ? 14 : 8;
+  return (K >= 12 && C >= 8) ? 10 : 8;
 }
 
 static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
@@ -2462,8 +2464,15 @@ static int mix_prefetch_setup(const fs_tuning& tune, bool use_quad, bool use_qmc
   // helpers, leads 4 / 6 / 8 / 12: 3.85 / 3.62 / 3.76 / 3.81 us per step, none: 4.40
   // (profiles/r04/mix_solve_helper_sweep.txt); with it (16 helpers at K = 16), leads 6 / 8 / 10
   // / 12 / 16: 2.70-2.72 / 2.58 / 2.62-2.63 / 2.65 / 2.66, and at N = 300 1.96 for 6 and 8
-  // (profiles/r04/qmc_lead_sweep.txt)
-  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : (use_qmc ? 8 : 16);
+  // (profiles/r04/qmc_lead_sweep.txt); at N = 800 (K = 13) 8 is faster (2.33 vs 2.38-2.40), at
+  // N = 520 (K = 9) 6 (2.08 vs 2.18-2.24, profiles/r04/qmc_lead_sweep2.txt): 8 from K = 12, as
+  // the first-poll delay's step (qmc_poll_delay)
+  int qmc_k = 0;
+  if (use_qmc) {
+    const int lw = 16 * qmc_nk(N, C);
+    qmc_k = (mix_ldn(N) + lw - 1) / lw;
+  }
+  const int lead = tune.mix_prefetch_lead > 0 ? tune.mix_prefetch_lead : (use_qmc ? (qmc_k >= 12 ? 8 : 6) : 16);
   if (h > 0 && d_ws && ws_bytes >= MC_ERR_BYTES) {
     pf.prog = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(d_ws) + ws_bytes - MC_ERR_BYTES + 128);
     pf.h = h;
