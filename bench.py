@@ -98,8 +98,12 @@ def parse(argv=None):
     ap.add_argument('--train-form', choices=['auto', 'split', 'pair', 'teams'], default='auto',
                     help="fs_tuning.train_form / split_teams: the local-training kernel form for parallel "
                          "clients (A/B runs)")
-    ap.add_argument('--launch-timeout', type=float, default=1800.0,
-                    help='--gpus N launcher: wall-clock bound on the workers (seconds; 0 = none)')
+    ap.add_argument('--launch-timeout', type=float, default=0.0,
+                    help='--gpus N launcher: wall-clock bound on the whole run (seconds; default 0 = none: a '
+                         'long but healthy run is never cut; exit code 124 when it trips)')
+    ap.add_argument('--teardown-timeout', type=float, default=300.0,
+                    help='--gpus N launcher: once a worker has exited 0, the seconds the others get to finish '
+                         '(a rank hung in a collective or in teardown); exit code 124 when it trips (0 = none)')
     ap.add_argument('--split-early', choices=['auto', 'off'], default='auto',
                     help="fs_tuning.split_early: the split form's early row issue (A/B runs)")
     a = ap.parse_args(argv)
@@ -123,15 +127,21 @@ def _free_port():
     return port
 
 
-def spawn(n, cmd=None, timeout=None):
+def spawn(n, cmd=None, timeout=None, teardown=None):
     """Start n worker processes of this script (one per GPU; ``cmd`` overrides the command,
     for tests), relay rank 0's stdout, and return the exit code: 0 only if every worker
-    exited 0.  A failed worker ends the others (they would wait forever in a collective), and
-    so does the wall-clock bound ``timeout`` (seconds; default --launch-timeout): a rank hung
-    in a collective or in teardown after rank 0 printed its line must not hold the launcher
-    forever -- the workers are terminated, then killed, and the exit code is 124."""
-    if timeout is None:
-        timeout = parse().launch_timeout if cmd is None else 1800.0
+    exited 0.  A failed worker ends the others (they would wait forever in a collective).
+    Two wall-clock bounds, each ending the workers (terminate, then kill) with exit code 124:
+    ``teardown`` (default --teardown-timeout, 300 s) counts from the first worker that exits 0
+    -- a rank hung in a collective or in teardown after the others finished must not hold the
+    launcher forever -- and ``timeout`` (default --launch-timeout: none) bounds the whole run,
+    so a long but healthy run (large --steps, --fedamw-rounds) is never cut by default."""
+    if timeout is None or teardown is None:
+        a = parse() if cmd is None else None
+        if timeout is None:
+            timeout = a.launch_timeout if a is not None else 0.0
+        if teardown is None:
+            teardown = a.teardown_timeout if a is not None else 300.0
     cmd = cmd or [sys.executable, '-u', os.path.abspath(__file__)] + sys.argv[1:]
     t_start = time.time()
     port = _free_port()
@@ -162,6 +172,7 @@ def spawn(n, cmd=None, timeout=None):
                 p.wait()
 
     rc = 0
+    t_first_done = None
     while any(p.poll() is None for p in procs):
         bad = [p for p in procs if p.poll() not in (None, 0)]
         if bad:
@@ -169,8 +180,13 @@ def spawn(n, cmd=None, timeout=None):
             print('bench: worker pid %d exited %d; stopping the others' % (bad[0].pid, rc), file=sys.stderr, flush=True)
             stop_all()
             break
-        if timeout and time.time() - t_start > timeout:
-            print('bench: workers still running after the %.0f s launch timeout; stopping them' % timeout,
+        now = time.time()
+        if t_first_done is None and any(p.poll() == 0 for p in procs):
+            t_first_done = now
+        late = ('launch', timeout) if timeout and now - t_start > timeout else (
+            ('teardown', teardown) if teardown and t_first_done is not None and now - t_first_done > teardown else None)
+        if late:
+            print('bench: workers still running after the %.0f s %s timeout; stopping them (exit 124)' % (late[1], late[0]),
                   file=sys.stderr, flush=True)
             stop_all()
             th.join(timeout=5)

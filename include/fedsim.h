@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 13
+#define FS_ABI_VERSION 14
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -131,6 +131,14 @@ int64_t fs_tuning_size(void);
 int fs_set_tuning(const fs_tuning* t);
 int fs_set_thread_tuning(const fs_tuning* t);
 int fs_get_tuning(fs_tuning* t);
+/* (ABI 14) the process-wide value alone (what fs_set_tuning last set), whatever the calling
+ * thread's override; and the calling thread's override: returns 1 and fills *t if one is
+ * set, 0 (and *t = all-zero) if not.  A binding that changes one field for a block of code
+ * reads the value it will restore from the layer it writes (the ADVICE round-4 fix: a
+ * process-wide set from a thread with an override neither copies that override into the
+ * process value nor is shadowed silently). */
+int fs_get_process_tuning(fs_tuning* t);
+int fs_get_thread_tuning(fs_tuning* t);
 
 /* ------------------------------------------------------------------------- *
  * Host: DataLoader shuffle replay.
@@ -162,16 +170,18 @@ int fs_libsvm_read(const char* path, int64_t n_rows, int64_t n_features, int zer
 
 /* ------------------------------------------------------------------------- *
  * Device: the same shuffle replay as fs_randperm_batch, on the GPU; d_seeds/d_n/d_off
- * are device arrays of npasses int64.  max_n MUST bound every n[i] (the device cannot
- * check it before choosing the form): max_n <= 64 runs one pass per LANE (64 passes per
- * wave, the MT state and the shuffle in registers / the lane's LDS row; a pass longer than
- * 64 there is written as the identity permutation -- memory-safe, not torch's draw);
- * larger max_n runs one wave per pass with an LDS-resident (max_n <= ~38K) or in-place
- * global-memory permutation.  Bit-identical to fs_randperm_batch.  Asynchronous on
- * `stream`.
+ * are device arrays of npasses int64.  max_n MUST bound every n[i] (the host chooses the
+ * form from it before the device sees n): max_n <= 64 runs one pass per LANE (64 passes per
+ * wave, the MT state and the shuffle in registers / the lane's LDS row); larger max_n runs
+ * one wave per pass with an LDS-resident (max_n <= ~38K) or in-place global-memory
+ * permutation.  Bit-identical to fs_randperm_batch.  Asynchronous on `stream`.
+ * (ABI 14) d_err (device, may be NULL): a pass with n[i] > max_n -- a caller breaking the
+ * contract -- is written as the identity permutation (memory-safe: no LDS row or buffer is
+ * overrun) and sets *d_err to 1 (sticky; the caller zeroes it once, reads it after the work
+ * and raises -- Shuffler.check_errors in engine.py).
  * ------------------------------------------------------------------------- */
 int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t* d_off, int64_t npasses,
-                       int64_t max_n, int32_t* d_out, void* stream);
+                       int64_t max_n, int32_t* d_out, uint32_t* d_err, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * Local training of N clients.  Replaces train_loop (tools.py:177-215) called

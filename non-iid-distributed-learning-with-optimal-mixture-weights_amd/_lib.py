@@ -20,11 +20,13 @@ _SIGS = {
     'fs_set_tuning': (C.c_int, [C.c_void_p]),
     'fs_set_thread_tuning': (C.c_int, [C.c_void_p]),
     'fs_get_tuning': (C.c_int, [C.c_void_p]),
+    'fs_get_process_tuning': (C.c_int, [C.c_void_p]),
+    'fs_get_thread_tuning': (C.c_int, [C.c_void_p]),
     'fs_randperm_batch': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     'fs_libsvm_scan': (C.c_int, [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     'fs_libsvm_read': (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
     'fs_randperm_device': (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
-                                     C.c_void_p]),
+                                     C.c_void_p, C.c_void_p]),
     'fs_local_train_plan': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int,
                                       C.c_int, C.c_void_p, C.c_void_p]),
     'fs_local_train': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -67,7 +69,7 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
@@ -143,52 +145,78 @@ def get_tuning():
     return {k: getattr(t, k) for k, _ in Tuning._fields_}
 
 
-def set_tuning(**fields):
-    """Set process-wide fs_tuning fields (the others keep their current values).  ``mix_solver``
-    may be a solver name ('quad', 'qmc', ...).  Returns the previous settings (a dict)."""
-    prev = get_tuning()
-    cur = dict(prev)
+def get_process_tuning():
+    """The process-wide fs_tuning (fs_set_tuning's value), whatever the calling thread's override."""
+    t = Tuning()
+    check(lib().fs_get_process_tuning(C.byref(t)), 'fs_get_process_tuning')
+    return {k: getattr(t, k) for k, _ in Tuning._fields_}
+
+
+def get_thread_tuning():
+    """The calling thread's override as a dict, or None when the thread has none."""
+    t = Tuning()
+    has = lib().fs_get_thread_tuning(C.byref(t))
+    if has < 0:
+        check(has, 'fs_get_thread_tuning')
+    return {k: getattr(t, k) for k, _ in Tuning._fields_} if has else None
+
+
+def _merged(base, fields):
+    cur = dict(base)
     for k, v in fields.items():
         if k not in cur:
             raise KeyError('fs_tuning has no field %r' % k)
         if k == 'mix_solver' and isinstance(v, str):
             v = 0 if v == 'auto' else SOLVERS[v]
         cur[k] = int(v)
-    t = Tuning(**cur)
-    check(lib().fs_set_tuning(C.byref(t)), 'fs_set_tuning')
+    return cur
+
+
+def set_tuning(**fields):
+    """Set process-wide fs_tuning fields (the others keep their current process-wide values,
+    never a thread override's).  ``mix_solver`` may be a solver name ('quad', 'qmc', ...).
+    Returns the previous process-wide settings (a dict).  A thread that holds an override
+    keeps using it: ``tuning`` below changes the override instead on such a thread."""
+    prev = get_process_tuning()
+    check(lib().fs_set_tuning(C.byref(Tuning(**_merged(prev, fields)))), 'fs_set_tuning')
     return prev
 
 
 def set_thread_tuning(fields=None):
     """fs_set_thread_tuning: an override for the launches the calling host thread enqueues
-    (``fields``: a dict over the process-wide defaults, solver names allowed), or None to drop
+    (``fields``: a dict over the all-default tuning, solver names allowed), or None to drop
     the thread's override."""
     if fields is None:
         check(lib().fs_set_thread_tuning(None), 'fs_set_thread_tuning')
         return
-    cur = {k: 0 for k, _ in Tuning._fields_}
-    for k, v in fields.items():
-        if k not in cur:
-            raise KeyError('fs_tuning has no field %r' % k)
-        if k == 'mix_solver' and isinstance(v, str):
-            v = 0 if v == 'auto' else SOLVERS[v]
-        cur[k] = int(v)
+    cur = _merged({k: 0 for k, _ in Tuning._fields_}, fields)
     check(lib().fs_set_thread_tuning(C.byref(Tuning(**cur))), 'fs_set_thread_tuning')
 
 
 class tuning:
     """Context manager: ``with _lib.tuning(mix_solver='qmc', mix_prefetch=-1): ...`` sets
-    fs_tuning fields for the block and restores the previous values after it."""
+    fs_tuning fields for the block and restores the previous values after it.  On a thread
+    without an override it changes the process-wide value (every thread without an override
+    sees it); on a thread that holds an override it changes that override (the layer the
+    thread's launches read) and restores it on exit -- the process-wide value is untouched."""
 
     def __init__(self, **fields):
         self.fields = fields
 
     def __enter__(self):
-        self.prev = set_tuning(**self.fields)
+        own = get_thread_tuning()
+        self.thread_prev = own
+        if own is not None:
+            set_thread_tuning(_merged(own, self.fields))
+        else:
+            self.prev = set_tuning(**self.fields)
         return self
 
     def __exit__(self, *exc):
-        set_tuning(**self.prev)
+        if self.thread_prev is not None:
+            set_thread_tuning(self.thread_prev)
+        else:
+            check(lib().fs_set_tuning(C.byref(Tuning(**self.prev))), 'fs_set_tuning')
         return False
 
 

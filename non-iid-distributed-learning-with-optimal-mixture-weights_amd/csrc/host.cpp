@@ -88,6 +88,19 @@ extern "C" int fs_get_tuning(fs_tuning* t) {
   return FS_OK;
 }
 
+extern "C" int fs_get_process_tuning(fs_tuning* t) {
+  if (!t) return fs::fail(FS_EINVAL, "fs_get_process_tuning: null pointer");
+  std::lock_guard<std::mutex> lk(fs::g_tune_m);
+  *t = fs::g_tune;
+  return FS_OK;
+}
+
+extern "C" int fs_get_thread_tuning(fs_tuning* t) {
+  if (!t) return fs::fail(FS_EINVAL, "fs_get_thread_tuning: null pointer");
+  *t = fs::t_tune_set ? fs::t_tune : fs_tuning{};
+  return fs::t_tune_set ? 1 : 0;
+}
+
 extern "C" const char* fs_last_error(void) { return fs::g_last_error.c_str(); }
 
 extern "C" int fs_randperm_batch(const int64_t* h_seeds, const int64_t* h_n, const int64_t* h_off, int64_t npasses,

@@ -83,18 +83,32 @@ __device__ void mt_twist(uint32_t* mt) {
   __syncthreads();
 }
 
+// a pass longer than the launch's max_n (a caller breaking the contract, include/fedsim.h): its
+// rows are written as the identity permutation (bounded, in global memory) and the error word
+// is set, so the host raises instead of training on a silently unshuffled pass
+__device__ __forceinline__ void rp_contract_broken(int32_t* dst, int n, int lane, int stride, uint32_t* err) {
+  for (int i = lane; i < n; i += stride) dst[i] = i;
+  if (err && lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool IN_LDS>
 __global__ __launch_bounds__(RP_THREADS) void randperm_kernel(const int64_t* __restrict__ seeds,
                                                              const int64_t* __restrict__ ns,
                                                              const int64_t* __restrict__ offs,
-                                                             int32_t* __restrict__ out) {
+                                                             int32_t* __restrict__ out, int64_t max_n,
+                                                             uint32_t* err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_rp[];
   uint32_t* mt = smem_rp;             // [624]
   uint32_t* rnd = mt + MT_N;          // [624]
   const int lane = threadIdx.x;
   const int pass = blockIdx.x;
-  const int n = (int)ns[pass];
+  const int64_t n64 = ns[pass];
   int32_t* dst = out + offs[pass];
+  if (n64 > max_n) {                  // (wave-uniform)
+    rp_contract_broken(dst, (int)n64, lane, RP_THREADS, err);
+    return;
+  }
+  const int n = (int)n64;
   int32_t* perm = IN_LDS ? reinterpret_cast<int32_t*>(rnd + MT_N) : dst;
   for (int i = lane; i < n; i += RP_THREADS) perm[i] = i;
   if (lane == 0) {
@@ -138,7 +152,7 @@ constexpr int RL_MAXN = 64;
 __global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __restrict__ seeds,
                                                            const int64_t* __restrict__ ns,
                                                            const int64_t* __restrict__ offs, int64_t npasses,
-                                                           int32_t* __restrict__ out) {
+                                                           int32_t* __restrict__ out, int max_n, uint32_t* err) {
   __shared__ int32_t perm_s[64][RL_MAXN + 1];
   const int lane = threadIdx.x;
   const int64_t pass = (int64_t)blockIdx.x * 64 + lane;
@@ -146,8 +160,10 @@ __global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __res
   const int n_req = live ? (int)ns[pass] : 0;
   // the contract (fedsim.h): every ns[pass] <= max_n; this form is chosen for max_n <= RL_MAXN.
   // A longer pass (a caller bug) must not shuffle into its neighbours' LDS rows: it is written
-  // as the identity permutation -- valid row indices, memory-safe, and not torch's draw
-  const int n = n_req <= RL_MAXN ? n_req : 0;
+  // as the identity permutation -- valid row indices, memory-safe -- and the error word is set
+  // (max_n <= RL_MAXN here)
+  const int n = n_req <= max_n ? n_req : 0;
+  if (n_req > max_n && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int32_t* perm = perm_s[lane];
   uint32_t lo[RL_MAXN], hi[RL_MAXN - 1];
   {
@@ -185,14 +201,14 @@ __global__ __launch_bounds__(64) void randperm_lanes_kernel(const int64_t* __res
 using namespace fs;
 
 extern "C" int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t* d_off, int64_t npasses,
-                                  int64_t max_n, int32_t* d_out, void* stream) {
+                                  int64_t max_n, int32_t* d_out, uint32_t* d_err, void* stream) {
   FS_REQUIRE(npasses >= 0 && max_n >= 0 && max_n < ((int64_t)1 << 31), "bad sizes");
   if (npasses == 0) return FS_OK;
   FS_REQUIRE(d_seeds && d_n && d_off && d_out, "null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (max_n <= RL_MAXN) {
     hipLaunchKernelGGL(randperm_lanes_kernel, dim3((unsigned)((npasses + 63) / 64)), dim3(64), 0, st, d_seeds, d_n,
-                       d_off, npasses, d_out);
+                       d_off, npasses, d_out, (int)max_n, d_err);
     FS_LAUNCH_CHECK();
     return FS_OK;
   }
@@ -205,10 +221,10 @@ extern "C" int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, co
       if (e != hipSuccess) return fail(FS_EHIP, std::string("fs_randperm_device: ") + hipGetErrorString(e));
     }
     hipLaunchKernelGGL(randperm_kernel<true>, dim3((unsigned)npasses), dim3(RP_THREADS), lds_full, st, d_seeds, d_n,
-                       d_off, d_out);
+                       d_off, d_out, max_n, d_err);
   } else {
     hipLaunchKernelGGL(randperm_kernel<false>, dim3((unsigned)npasses), dim3(RP_THREADS), lds_small, st, d_seeds, d_n,
-                       d_off, d_out);
+                       d_off, d_out, max_n, d_err);
   }
   FS_LAUNCH_CHECK();
   return FS_OK;

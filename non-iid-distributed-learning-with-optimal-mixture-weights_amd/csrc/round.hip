@@ -329,7 +329,8 @@ static int device_shuffle(fs_plan* p, const int64_t* h_seeds, int t) {
     FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * P, hipMemcpyHostToDevice, p->copy),
            "fs_plan_shuffle");
   const int64_t* seeds = p->seed_copy ? p->d_seed[k] : p->h_seed_dev[k];
-  const int rc = fs_randperm_device(seeds, p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], p->copy);
+  // (no error word: p->max_n is the maximum of the plan's own pass sizes)
+  const int rc = fs_randperm_device(seeds, p->d_pass, p->d_pass + P, P, p->max_n, p->d_perm[s], nullptr, p->copy);
   if (rc != FS_OK) return rc;
   FS_HIP(hipEventRecord(p->seed_read[k], p->copy), "fs_plan_shuffle");
   p->seed_pending[k] = true;
@@ -399,8 +400,9 @@ static int launch_chunk(fs_plan* p) {
       FS_HIP(hipMemcpyAsync(p->d_seed[k], p->h_seed[k], sizeof(int64_t) * nr * P, hipMemcpyHostToDevice, p->copy),
              "fs_plan_shuffle");
     const int64_t* seeds = p->seed_copy ? p->d_seed[k] : p->h_seed_dev[k];
+    // (no error word: the plan's max_n is the maximum of its own pass sizes, so no pass exceeds it)
     const int rc = fs_randperm_device(seeds, p->d_pass_chunk, p->d_pass_chunk + KP, nr * P, p->max_n, p->d_perm[s],
-                                      p->copy);
+                                      nullptr, p->copy);
     if (rc != FS_OK) return rc;
   }
   FS_HIP(hipEventRecord(p->seed_read[k], p->copy), "fs_plan_shuffle");

@@ -64,9 +64,12 @@ class Shuffler:
     trains (``prepare``), ordered by events: a slot is rewritten only after the kernel
     that consumed it has finished (``consumed``), and read only after it is ready."""
 
-    def __init__(self, ns, offs, size, device):
+    def __init__(self, ns, offs, size, device, max_n=None):
         self.P = int(len(ns))
-        self.max_n = int(np.max(ns)) if self.P else 0
+        # the launch contract (include/fedsim.h): max_n bounds every pass; a caller may pass a
+        # smaller value only to exercise the error path (check_errors then raises)
+        self.max_n = int(max_n) if max_n is not None else (int(np.max(ns)) if self.P else 0)
+        self.err = torch.zeros(_lib.ERR_BLOCK // 4, dtype=torch.int32, device=device)
         self.n_dev = torch.as_tensor(np.asarray(ns, dtype=np.int64)).to(device)
         self.off_dev = torch.as_tensor(np.asarray(offs, dtype=np.int64)).to(device)
         self.bufs = [torch.empty(max(1, int(size)), dtype=torch.int32, device=device) for _ in range(2)]
@@ -94,7 +97,8 @@ class Shuffler:
             if self.P:
                 _lib.check(_lib.lib().fs_randperm_device(_lib.ptr(self.seed_dev[slot]), _lib.ptr(self.n_dev),
                                                          _lib.ptr(self.off_dev), self.P, self.max_n,
-                                                         _lib.ptr(self.bufs[slot]), _lib.stream_ptr(stream)),
+                                                         _lib.ptr(self.bufs[slot]), _lib.ptr(self.err),
+                                                         _lib.stream_ptr(stream)),
                            'fs_randperm_device')
             ready = torch.cuda.Event()
             ready.record(stream)
@@ -115,6 +119,14 @@ class Shuffler:
         """Synchronous-order convenience: prepare on the current stream and return the buffer."""
         self.prepare(seeds, slot)
         return self.acquire(slot)
+
+    def check_errors(self):
+        """Raise if a pass broke the max_n contract (it was written unshuffled; synchronises)."""
+        err = int(self.err[0].item())
+        if err:
+            self.err.zero_()
+            raise _lib.FedsimError('fs_randperm_device: a pass is longer than max_n = %d; it was written as the '
+                                   'identity permutation (code %d)' % (self.max_n, err))
 
 
 def _check_ws_error(ws, what):
@@ -191,8 +203,11 @@ class LocalTrainer:
         return self._shuffler
 
     def check_errors(self):
-        """Raise if a split-client launch reported a broken hand-off (synchronises)."""
+        """Raise if a split-client launch reported a broken hand-off, or a shuffle of this
+        trainer's passes broke its length contract (synchronises)."""
         _check_ws_error(self.ws, 'fs_local_train')
+        if self._shuffler is not None:
+            self._shuffler.check_errors()
 
     def upload_perms(self, seeds, slot=0, stream=None):
         """seeds: [N*E] sampler seeds of one round's local training passes (client-major);
@@ -371,6 +386,11 @@ class Mixture:
         validation passes (one per inner epoch), or None when ``prepare`` already enqueued
         them into ``slot``.  ``z=False`` reuses Z from the previous call (W_all unchanged)."""
         L = _lib.lib()
+        if z and self.blocks > 1:
+            # fs_mix_z writes the standard [n_val][C][ldN] layout; fs_mix_solve_blocked would
+            # read it as rank blocks (ADVICE round 4)
+            raise ValueError('Mixture.solve(z=True) with blocks=%d: Z must come from the rank-block '
+                             'all-gather (dist.allgather_z(blocked=True)), then solve(z=False)' % self.blocks)
         if z:
             _lib.check(L.fs_mix_z(_lib.ptr(W_all), _lib.ptr(self.f.phi), self.f.ld, self.N, self.C, self.nv,
                                   _lib.ptr(self.Z), _lib.stream_ptr()), 'fs_mix_z')

@@ -185,9 +185,10 @@ class Federation:
                 p0 = torch.zeros(Ns, dtype=torch.float32)
                 p0[torch.from_numpy(self.pos)] = self.p_all
                 self.mixture = engine.Mixture(Xv, yv, D, C, Ns, Bv, p0, dev, ld)
-                # the qmc solver reads the all-gathered rank blocks as they land (no layout copy)
-                if nranks > 1 and self.mixture.blocked_covers(R):
-                    self.mixture.blocks = nranks
+                # the qmc solver reads the all-gathered rank blocks as they land (no layout copy);
+                # which layout to gather is decided again every round, right before the
+                # all-gather (round()), under the tuning the enqueueing thread has then
+                self.nranks = nranks
                 self.Z_local = torch.empty(self.mixture.nv, C * self.L, device=dev, dtype=torch.float32)
                 lo = self.rank * self.L
                 self.p_slice = lambda p: p[lo:lo + len(mine)]
@@ -292,6 +293,11 @@ class Federation:
             # tools.py:435-453 sharded: this rank's Z columns, one all-gather, the replicated
             # p-solve, then this rank's partial aggregate with its learned p and one all-reduce
             self.p_hist[t].copy_(self.mixture.p[self.pos_dev])
+            # the blocked layout only where fs_mix_solve_blocked covers the shape under THIS
+            # thread's tuning now (a tuning change between rounds, or a round
+            # enqueued from another thread, must not leave a blocked Z for a solver that
+            # cannot read it)
+            self.mixture.blocks = (self.nranks if self.nranks > 1 and self.mixture.blocked_covers(self.R) else 1)
             timed('z', lambda: self.mixture.z_block(self.trainer.W_out, self.L, self.Z_local))
             timed('z_allgather', lambda: dist.allgather_z(self.Z_local, self.C, self.mixture.Z,
                                                           blocked=self.mixture.blocks > 1))

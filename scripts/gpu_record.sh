@@ -1,8 +1,8 @@
 #!/bin/bash
-# round-4 record: full GPU suite (verbose), smoke(), then the default bench line twice
+# round record: full GPU suite (verbose), smoke(), then the default bench line twice
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-R=${1:-r04final}
+R=${1:-record}
 mkdir -p gpurun_out/$R
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
   > gpurun_out/$R/gpu_tests.log 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/$R/gpu_tests.log; exit 1; }

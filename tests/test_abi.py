@@ -111,3 +111,49 @@ def test_tuning_threading_contract():
         assert 'mix_poll_delay' in L.fs_last_error().decode()
     finally:
         _lib.set_tuning(**prev)
+
+
+def test_tuning_context_on_a_thread_with_an_override():
+    """``with _lib.tuning(...)`` on a thread that holds an override changes that
+    override (the layer the thread's launches read) and restores it on exit; the process-wide
+    value is neither overwritten with the override's fields nor changed.  set_tuning from such a
+    thread changes only the process-wide value.  Host-only."""
+    import threading
+    prev = _lib.set_tuning(mix_solver='quad', mix_poll_delay=3)
+    try:
+        seen = {}
+
+        def worker():
+            _lib.set_thread_tuning({'mix_solver': 'qmc', 'split_poll_delay': 5})
+            with _lib.tuning(mix_prefetch=-1):
+                seen['inside'] = _lib.get_tuning()
+                seen['inside_process'] = _lib.get_process_tuning()
+            seen['after'] = _lib.get_tuning()
+            seen['thread_after'] = _lib.get_thread_tuning()
+            old = _lib.set_tuning(mix_poll_delay=7)          # process-wide only
+            seen['set_prev'] = old
+            seen['own_after_set'] = _lib.get_tuning()
+            _lib.set_tuning(**old)
+            _lib.set_thread_tuning(None)
+            seen['dropped'] = _lib.get_thread_tuning()
+
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+        assert seen['inside']['mix_solver'] == _lib.SOLVERS['qmc'] and seen['inside']['mix_prefetch'] == -1
+        assert seen['inside']['split_poll_delay'] == 5
+        assert seen['inside_process']['mix_solver'] == _lib.SOLVERS['quad']
+        assert seen['inside_process']['mix_prefetch'] == 0 and seen['inside_process']['split_poll_delay'] == 0
+        assert seen['after']['mix_prefetch'] == 0 and seen['after']['mix_solver'] == _lib.SOLVERS['qmc']
+        assert seen['thread_after'] == seen['after']
+        assert seen['set_prev']['mix_solver'] == _lib.SOLVERS['quad'] and seen['set_prev']['mix_poll_delay'] == 3
+        assert seen['own_after_set']['mix_poll_delay'] == 0                 # the override still wins
+        assert seen['dropped'] is None
+        proc = _lib.get_process_tuning()
+        assert proc['mix_solver'] == _lib.SOLVERS['quad'] and proc['mix_poll_delay'] == 3
+        assert _lib.get_thread_tuning() is None
+        with _lib.tuning(mix_prefetch=-1):                  # no override here: process-wide
+            assert _lib.get_process_tuning()['mix_prefetch'] == -1
+        assert _lib.get_process_tuning()['mix_prefetch'] == 0
+    finally:
+        _lib.set_tuning(**prev)

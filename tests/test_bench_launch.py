@@ -62,6 +62,24 @@ def test_spawn_launch_timeout(tmp_path, capfd):
     assert '{}' in capfd.readouterr().out
 
 
+def test_spawn_teardown_timeout(tmp_path, capfd):
+    """The default bound counts only from the first worker that exits 0: a rank still running
+    that long after rank 0 finished is stopped (124); a long but healthy run with no finished
+    rank is not cut (no whole-run bound by default)."""
+    w = tmp_path / 'w.py'
+    w.write_text('import os, sys, time\nif os.environ["RANK"] == "0":\n    print("{}", flush=True)\n    sys.exit(0)\n'
+                 'time.sleep(600)\n')
+    import time
+    t0 = time.time()
+    assert bench.spawn(2, [sys.executable, str(w)], teardown=2.0) == 124
+    assert time.time() - t0 < 60
+    assert '{}' in capfd.readouterr().out
+    slow = tmp_path / 'slow.py'
+    slow.write_text('import time\ntime.sleep(4)\nprint("{}", flush=True)\n')
+    assert bench.spawn(2, [sys.executable, str(slow)], teardown=2.0) == 0
+    assert bench.parse([]).launch_timeout == 0.0
+
+
 def test_gpus_must_match_world_size(monkeypatch):
     monkeypatch.setenv('WORLD_SIZE', '2')
     args = bench.parse(['--gpus', '4'])

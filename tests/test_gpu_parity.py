@@ -929,6 +929,39 @@ def test_device_randperm_short_passes_mixed(amd):
         np.testing.assert_array_equal(host[offs[i]:offs[i] + ns[i]], torch.randperm(int(ns[i]), generator=g).numpy())
 
 
+@pytest.mark.parametrize('max_n,long_n', [(64, 65), (40, 41), (512, 600), (512, 50000)])
+def test_device_randperm_contract_violation_raises(amd, max_n, long_n):
+    """a pass longer than the launch's max_n (a caller breaking the
+    fs_randperm_device contract) is written as the identity permutation -- memory-safe, both
+    forms (one lane per pass at max_n <= 64, one wave per pass above) -- and sets the error word,
+    so check_errors raises FedsimError instead of training on a silently unshuffled pass.  The
+    passes that keep the contract are still torch's draws."""
+    dev = torch.device('cuda')
+    torch.manual_seed(max_n)
+    P = 7
+    seeds = amd.rng.draw_pass_seeds(P)
+    ns = np.full(P, min(max_n, 33), np.int64)
+    ns[3] = long_n
+    offs = np.concatenate([[0], np.cumsum(ns)[:-1]]).astype(np.int64)
+    total = int(ns.sum())
+    sh = amd.engine.Shuffler(ns, offs, total, dev, max_n=max_n)
+    out = sh.run(seeds).cpu().numpy()
+    np.testing.assert_array_equal(out[offs[3]:offs[3] + long_n], np.arange(long_n, dtype=np.int32))
+    ok = np.ones(P, bool)
+    ok[3] = False
+    host = np.empty(total, np.int32)
+    amd.rng.randperms(seeds, ns, offs, host)
+    for i in np.flatnonzero(ok):
+        np.testing.assert_array_equal(out[offs[i]:offs[i] + ns[i]], host[offs[i]:offs[i] + ns[i]])
+    with pytest.raises(amd.lib.FedsimError, match='longer than max_n'):
+        sh.check_errors()
+    sh.check_errors()                                   # cleared: a second check passes
+    ns[3] = min(max_n, 33)                              # a clean launch on the same shuffler
+    sh2 = amd.engine.Shuffler(ns, offs, total, dev, max_n=max_n)
+    sh2.run(seeds)
+    sh2.check_errors()
+
+
 @pytest.mark.parametrize('N', [300, 1000])
 def test_fedamw_dropin_many_clients_vs_oracle(amd, N):
     """The FedAMW drop-in end to end with more clients than any single-workgroup p-solver
