@@ -95,8 +95,8 @@ def parse(argv=None):
     ap.add_argument('--no-fedamw-leg', action='store_true', help='skip the FedAMW object of the config-2 line')
     ap.add_argument('--fedamw-rounds', type=int, default=2, help='timed FedAMW rounds of the config-2 leg')
     ap.add_argument('--no-legs', action='store_true', help='skip the config 3/4/5 objects of the default line')
-    ap.add_argument('--train-form', choices=['auto', 'split', 'pair', 'teams'], default='auto',
-                    help="fs_tuning.train_form / split_teams: the local-training kernel form for parallel "
+    ap.add_argument('--train-form', choices=['auto', 'split', 'pair', 'teams', 'pipe'], default='auto',
+                    help="fs_tuning.train_form / split_teams / split_pipe: the local-training kernel form for parallel "
                          "clients (A/B runs)")
     ap.add_argument('--launch-timeout', type=float, default=0.0,
                     help='--gpus N launcher: wall-clock bound on the whole run (seconds; default 0 = none: a '
@@ -486,7 +486,8 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                      'mfma_busy': (rec or {}).get('mfma_busy'),
                      'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes, 'group_width': fed.trainer.width,
                      'form': 'pair' if fed.trainer.pair else ('teams' if fed.trainer.teams else
-                                                              ('split' if fed.trainer.G > 1 else 'single'))},
+                                                              ('pipe' if fed.trainer.pipe else
+                                                               ('split' if fed.trainer.G > 1 else 'single')))},
         'final_test_acc': float(ta[fed.t - 1]),
     }
     if fedamw:
@@ -537,8 +538,9 @@ def worker(args):
     import fedamw_amd  # noqa: F401
     ws, rank, dev, dinfo = setup_rank(args)
     from fedamw_amd import _lib as flib
-    flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2, 'teams': 1}[args.train_form],
-                    split_teams={'auto': 0, 'split': -1, 'pair': -1, 'teams': 1}[args.train_form],
+    flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2, 'teams': 1, 'pipe': 1}[args.train_form],
+                    split_teams={'auto': 0, 'split': -1, 'pair': -1, 'teams': 1, 'pipe': -1}[args.train_form],
+                    split_pipe={'auto': 0, 'split': -1, 'pair': -1, 'teams': -1, 'pipe': 1}[args.train_form],
                     split_early={'auto': 0, 'off': -1}[args.split_early])
     wl = {k: getattr(args, k) for k in ('algo', 'clients', 'rows', 'D', 'C', 'test', 'shape')}
     wl['config'] = args.config

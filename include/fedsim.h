@@ -98,6 +98,8 @@ const char* fs_last_error(void);
  *   split_poll_delay   (ABI 13) split form: s_sleep(1) units between a step's publish and its
  *                      first poll: 0 = by width (16 at G >= 8 with parallel clients, else
  *                      none), -1 = none, n > 0 = n; bitwise the same results
+ *   split_pipe         (ABI 14) fs_local_train_plan's choice of the pipe form (FS_G_PIPE):
+ *                      0 = by shape, 1 = wherever it fits (G = ld / 1024), -1 = never
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -125,6 +127,7 @@ typedef struct fs_tuning {
   int split_teams;
   int mix_poll_delay;
   int split_poll_delay;
+  int split_pipe;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -219,6 +222,12 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              teams of 4 that train two clients at once with team-local barriers, so one
  *              team's hand-off and softmax run beside the other team's MFMAs (the split
  *              arithmetic with 4 waves per slice: within the fp32 tolerance of the split form).
+ *              G | FS_G_PIPE (ABI 14, ld == 1024 G with G = 2, 4 or 8, 16 < B <= 32, C <= 16, no
+ *              prox term; parallel or chained clients): the "pipe" form -- the split form with
+ *              each step's hand-off pipelined by 16-row tile (one tile's partner round trip under
+ *              the other tile's forward or backward MFMAs, the softmax per wave in registers, two
+ *              barriers per step); the same arithmetic in the same order as the split form at
+ *              width G (bitwise the same results).
  *              fs_local_train_plan: *G_out on entry is a request (0 = planner's choice, 1 =
  *              one workgroup per client, 2..16 = that split width if the shape allows it,
  *              G | FS_G_PAIR = the pair form, G | FS_G_TEAMS = the team form at that width
@@ -227,6 +236,7 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  * ------------------------------------------------------------------------- */
 #define FS_G_PAIR 256
 #define FS_G_TEAMS 512
+#define FS_G_PIPE 1024
 int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64_t max_en, int chained, int prox,
                         int* G_out, int64_t* ws_bytes_out);
 int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,

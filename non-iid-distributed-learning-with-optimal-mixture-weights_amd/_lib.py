@@ -74,6 +74,7 @@ ABI_VERSION = 14
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
 G_TEAMS = 512            # fs_local_train_plan: G | G_TEAMS = the team form at width G (ABI 13)
+G_PIPE = 1024            # fs_local_train_plan: G | G_PIPE = the pipelined split form at width G (ABI 14)
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
 SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc', 10: 'bin'}
 SOLVERS = {v: k for k, v in SOLVER_NAMES.items() if k}
@@ -86,7 +87,7 @@ class Tuning(C.Structure):
                 ('inject_timeout', C.c_int), ('train_form', C.c_int),
                 ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int),
                 ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int),
-                ('mix_poll_delay', C.c_int), ('split_poll_delay', C.c_int)]
+                ('mix_poll_delay', C.c_int), ('split_poll_delay', C.c_int), ('split_pipe', C.c_int)]
 
 
 class PlanDesc(C.Structure):
@@ -238,7 +239,8 @@ def stream_ptr(stream=None):
 
 # the device sources each measured kernel is compiled from (its own file + the headers it includes)
 KERNEL_SOURCES = {
-    'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_pair.hip', 'split_common.h', 'common.h',
+    'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_pair.hip', 'local_train_pipe.hip',
+                    'split_common.h', 'common.h',
                     'eval_rows.h', 'lanes.h'),
     'mix_solve': ('mixture.hip', 'common.h', 'lanes.h'),
     'mix_z': ('mix_z.hip', 'common.h'),

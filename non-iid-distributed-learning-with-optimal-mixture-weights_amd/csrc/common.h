@@ -79,6 +79,8 @@ int local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const 
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
 // pair-client launcher (local_train_pair.hip): G workgroups per group, two clients per group
 int launch_local_train_pair(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
+// pipelined split launcher (local_train_pipe.hip): G workgroups per client, hand-off by row tile
+int launch_local_train_pipe(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
 
 // ---- device helpers ----------------------------------------------------------
 typedef float floatx4 __attribute__((ext_vector_type(4)));

@@ -422,8 +422,9 @@ int fs::local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, co
     P.fuse_part = fuse->part;
   }
   if (G > 1) {
-    const int rc = (G & FS_G_PAIR) ? launch_local_train_pair(P, G & (FS_G_PAIR - 1), d_ws, ws_bytes, st)
-                                   : launch_local_train_split(P, G, d_ws, ws_bytes, st);
+    const int rc = (G & FS_G_PIPE)   ? launch_local_train_pipe(P, G & (FS_G_PAIR - 1), d_ws, ws_bytes, st)
+                   : (G & FS_G_PAIR) ? launch_local_train_pair(P, G & (FS_G_PAIR - 1), d_ws, ws_bytes, st)
+                                     : launch_local_train_split(P, G, d_ws, ws_bytes, st);
     if (rc != FS_OK) return rc;
     FS_LAUNCH_CHECK();
     return FS_OK;

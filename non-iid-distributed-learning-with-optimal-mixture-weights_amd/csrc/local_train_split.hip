@@ -753,6 +753,7 @@ static unsigned split_spin_limit() {
   if (t.inject_timeout) return 0u;
   return t.spin_limit ? t.spin_limit : SP_SPIN_LIMIT;
 }
+unsigned split_spin_bound() { return split_spin_limit(); }
 
 template <int RT, int G, bool PROX, int EARLY, int TEAMS>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
@@ -852,6 +853,12 @@ int launch_local_train_split(const LTParams& P, int Gf, void* ws, int64_t ws_byt
 
 int split_idle_cus(int N, int C, int B, int64_t ld, int G, int chained) {
   const int NT = (int)(ld >> 6);
+  if (G & FS_G_PIPE) {
+    const int g = G & (FS_G_PAIR - 1);
+    const int cus = device_cus();
+    if (chained || cus <= 0 || !pipe_fits(C, B, NT, g, 0)) return 0;
+    return std::max(0, cus - pipe_groups(N, g, 0, cus) * g);
+  }
   if (G & FS_G_PAIR) {
     const int g = G & (FS_G_PAIR - 1);
     const int cus = device_cus();
@@ -887,6 +894,24 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   const int cus = device_cus();
   if (want == 1 || C > 16 || B > 32 || cus <= 0) return FS_OK;
   const int NT = (int)(ld >> 6);
+  // an explicit pipe request
+  if (want & FS_G_PIPE) {
+    const int g = want & (FS_G_PAIR - 1);
+    if (pipe_fits(C, B, NT, g, prox) && g <= cus) {
+      *G_out = g | FS_G_PIPE;
+      *ws_bytes_out = pipe_ws_bytes(N, g, chained, cus);
+      return FS_OK;
+    }
+  }
+  // the pipe form by tuning (fs_tuning.split_pipe = 1: wherever it fits; 0 = by shape, -1 = never)
+  if (!(want > 1 && want < FS_G_PAIR) && tuning().split_pipe > 0 && NT % 16 == 0) {
+    const int g = NT / 16;
+    if (pipe_fits(C, B, NT, g, prox) && g <= cus) {
+      *G_out = g | FS_G_PIPE;
+      *ws_bytes_out = pipe_ws_bytes(N, g, chained, cus);
+      return FS_OK;
+    }
+  }
   // an explicit team request
   if (want & FS_G_TEAMS) {
     const int g = want & (FS_G_PAIR - 1);

@@ -18,6 +18,10 @@ unsigned exchange_generation(const void* ws, bool long_launch);
 
 // the pair form (local_train_pair.hip)
 bool pair_fits(int C, int B, int NT, int G);
+// the pipe form (local_train_pipe.hip)
+bool pipe_fits(int C, int B, int NT, int G, int prox);
+int pipe_groups(int N, int G, int chained, int cus);
+int64_t pipe_ws_bytes(int N, int G, int chained, int cus);
 int pair_groups(int N, int G, int cus);
 int64_t pair_ws_bytes(int N, int G, int B, int cus);
 

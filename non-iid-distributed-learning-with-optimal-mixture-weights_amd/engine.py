@@ -149,7 +149,7 @@ class LocalTrainer:
     mode as persistent groups over the clients -- two clients per group in the pair form
     (G | _lib.G_PAIR) where the shape allows it -- in chained mode as one group walking the
     chain); 1 forces one workgroup per client, G a split width, G | _lib.G_PAIR the pair form,
-    G | _lib.G_TEAMS the team form."""
+    G | _lib.G_TEAMS the team form, G | _lib.G_PIPE the pipelined split form."""
 
     def __init__(self, feats, C, B, E, split=None, chained=False, rows=None, prox=False):
         self.f = feats
@@ -182,6 +182,7 @@ class LocalTrainer:
         self.G = int(g.value)                       # as the ABI takes it (G | G_PAIR: the pair form)
         self.pair = bool(self.G & _lib.G_PAIR)
         self.teams = bool(self.G & _lib.G_TEAMS)
+        self.pipe = bool(self.G & _lib.G_PIPE)
         self.width = self.G & (_lib.G_PAIR - 1)     # workgroups per client group
         self.ws = (torch.zeros(max(2 * _lib.ERR_BLOCK, int(wsb.value)), dtype=torch.uint8, device=dev)
                    if self.G > 1 else None)

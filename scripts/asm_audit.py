@@ -1,8 +1,8 @@
-"""Audit the pair kernel's hand-counted loads in the built gfx950 assembly.
+"""Audit the hand-counted loads of the pair and pipe kernels in the built gfx950 assembly.
 
-    python scripts/asm_audit.py [path/to/local_train_pair.s]
+    python scripts/asm_audit.py [pair|pipe] [path/to/built.s]
 
-local_train_pair.hip issues its in-loop loads as inline asm (tagged `; pr-row`, `; pr-idx`,
+local_train_pair.hip (and local_train_pipe.hip, with the same tags) issues its in-loop loads as inline asm (tagged `; pr-row`, `; pr-idx`,
 `; pr-poll`) that hipcc does not track, and names each destination in a `; pr-own <reg>`
 statement after the counted wait that retires it (cdna_hip_programming.md 5.7 item 1,
 form ii).  Between a load and that statement no other instruction may read, write, copy or
@@ -17,8 +17,9 @@ import sys
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, 'non-iid-distributed-learning-with-optimal-mixture-weights_amd', 'csrc',
-                   'local_train_pair.hip')
+CSRC = os.path.join(ROOT, 'non-iid-distributed-learning-with-optimal-mixture-weights_amd', 'csrc')
+KERNELS = {'pair': ('local_train_pair.hip', r'^_Z\w*local_train_pair_kernel\w*:'),
+           'pipe': ('local_train_pipe.hip', r'^_Z\w*local_train_pipe_kernel\w*:')}
 REG = re.compile(r'\bv\[(\d+):(\d+)\]|\bv(\d+)\b')
 
 
@@ -124,12 +125,15 @@ def audit_function(name, lines):
 
 
 def main():
-    path = sys.argv[1] if len(sys.argv) > 1 else '/tmp/local_train_pair.s'
-    if len(sys.argv) <= 1:
+    args = sys.argv[1:]
+    kind = args.pop(0) if args and args[0] in KERNELS else 'pair'
+    src, fre = KERNELS[kind]
+    path = args[0] if args else '/tmp/local_train_%s.s' % kind
+    if not args:
         subprocess.check_call(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '--offload-arch=gfx950',
-                               '-munsafe-fp-atomics', '--cuda-device-only', '-S', SRC, '-o', path])
+                               '-munsafe-fp-atomics', '--cuda-device-only', '-S', os.path.join(CSRC, src), '-o', path])
     text = open(path).read().split('\n')
-    funcs = [(i, l.split(':')[0]) for i, l in enumerate(text) if re.match(r'^_Z\w*local_train_pair_kernel\w*:', l)]
+    funcs = [(i, l.split(':')[0]) for i, l in enumerate(text) if re.match(fre, l)]
     total_bad = total = 0
     for fi, (start, name) in enumerate(funcs):
         end = next(i for i in range(start, len(text)) if text[i].startswith('.Lfunc_end'))
