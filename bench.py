@@ -33,6 +33,9 @@ Extra objects on the JSON line:
                 round) timed on this host (rank 0, N = 1 only) on a bounded sample.
   fedamw        (config 2, one GPU) the other half of config 2 -- "FedAvg vs optimal mixture
                 weights": FedAMW rounds on the same clients plus 128 validation rows each.
+  config1       (default run, one GPU) exp.py's FedAMW on 10 chained a9a-shaped Dirichlet(0.01)
+                clients, D = 2000, C = 2, R = 100: ms per round, the bin p-solve's us per step, and
+                the numpy oracle's round on the host.
   config4 / config3 / config5
                 (default run) the >= 1000-client BASELINE configs, each with its own rounds,
                 ms_per_round, client-rounds/s, roofline and cpu_baseline; config 5 adds the
@@ -400,6 +403,104 @@ def fedamw_leg(d, wl, dev, R, rounds, warmup=1):
             'n_val': nv, 'inner_epochs': R, 'rounds_timed': rounds}
 
 
+def config1_leg(dev, rounds=10, warmup=2, cpu_budget=3.0):
+    """BASELINE config 1 -- exp.py's FedAMW on a9a split across 10 non-IID clients
+    (/root/reference/exp.py:22-143 -> tools.py:413-463): exp.py's data prep (a9a-shaped synthetic
+    rows -- no LIBSVM file travels -- Dirichlet(0.01) partition, full-batch pass, RFF map D = 2000,
+    20/80 validation split) and FedAMW with exp.py's positional arguments and get_parameter('a9a')
+    (default branch; lr_p = 1e-3, stated in experiment.py), CHAINED clients (the reference's
+    semantics: one model walks the 10 clients), R = 100 (40,700 p-SGD steps per round with the
+    `bin` p-solver).  Rounds ``warmup`` .. ``warmup + rounds`` of the 100 are timed (the LR
+    schedule is the run's own); one GPU (a chain does not shard: replicas only).  CPU: the numpy
+    oracle's whole round (the chained local training, the p-solve's R passes on the pooled
+    validation set, the aggregate and the test evaluation), timed in full when it fits
+    ``cpu_budget``, else with the p-SGD passes sampled and extrapolated (stated)."""
+    import torch
+    import fedamw_amd
+    from fedamw_amd import experiment
+    from fedamw_amd.functions import tools
+    from fedamw_amd.functions.optimal_parameters import get_parameter
+    P = get_parameter('a9a')
+    D, N, R, E, B = 2000, 10, 100, 2, 32
+    lr, lam, lr_p = P['lr'], P['lambda_reg'], P.get('lr_p', 1e-3)
+    torch.manual_seed(100)
+    np.random.seed(100)
+    d = experiment.prepare('a9a', D, N, 0.01, P, '/nonexistent/', verbose=False)
+    C = d['num_classes']
+    fed = tools.Federation('fedamw', d['X_train'], d['y_train'], d['X_test'], d['y_test'], d['validloader'],
+                           'classification', C, D, lr, E, B, False, 0.0, True, lam, R, lr_p, 'sequential',
+                           verbose=False)
+    for _ in range(warmup):
+        fed.round()
+    torch.cuda.synchronize()
+    fed.events = []
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        fed.round()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tr, tl, ta = fed.results()
+    nv = fed.mixture.nv
+    steps = R * ((nv + 15) // 16)
+    solve_ms, train_ms, z_ms = (phase_ms(fed.events, k) for k in ('solve', 'train', 'z'))
+    sizes = [int(len(y)) for y in d['y_train']]
+    out = {'workload': 'config 1: exp.py FedAMW, a9a-shaped (synthetic), %d Dirichlet(0.01) clients (%d..%d rows, '
+                       'sum %d), RFF D=%d, C=%d, E=%d, B=%d, round=%d, chained clients (reference semantics), '
+                       '%d validation rows' % (N, min(sizes), max(sizes), sum(sizes), D, C, E, B, R, nv),
+           'value': N * rounds / el, 'unit': 'client-rounds/s', 'ms_per_round': 1e3 * el / rounds,
+           'rounds_timed': rounds, 'warmup': warmup, 'scaling': 'replicas only (a chain does not shard)',
+           'train_ms': train_ms, 'z_gemm_ms': z_ms, 'p_solve_ms': solve_ms, 'p_solve_steps': steps,
+           'p_solve_us_per_step': 1e3 * solve_ms / steps if solve_ms else None,
+           'p_solver': fedamw_amd._lib.SOLVER_NAMES.get(fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
+           'local_train_group_width': fed.trainer.width, 'final_test_acc': float(ta[fed.t - 1]),
+           'context': 'BASELINE.md: the reference CPU path runs this round in 20.0 s = 0.50 client-rounds/s on '
+                      '8 Xeon cores (survey container; not a published number)'}
+    if cpu_budget > 0:
+        from oracle import fedsim_oracle as O
+        from threadpoolctl import threadpool_info
+        Xs = [_np(x) for x in d['X_train']]
+        ys = [_np(y).astype(np.int64) for y in d['y_train']]
+        Xv, yv = _np(d['X_val']).astype(np.float32), _np(d['y_val']).astype(np.int64)
+        Xt, yt = _np(d['X_test']).astype(np.float32), _np(d['y_test']).astype(np.int64)
+        state = torch.get_rng_state()
+        torch.manual_seed(1234)
+        W = O.mlp_init(D, C)
+        a = time.perf_counter()
+        Ws, _ = O._chain(Xs, ys, W, lr, E, B, False, 0.0, True, lam)
+        t_train = time.perf_counter() - a
+        a = time.perf_counter()
+        Z = np.einsum('ncd,vd->ncv', np.stack(Ws).astype(np.float32), Xv, optimize=True)
+        t_z = time.perf_counter() - a
+        p = np.full(N, 1.0 / N, np.float32)
+        spp = (nv + 15) // 16
+        left = max(0.2, cpu_budget - t_train - t_z)
+        a = time.perf_counter()
+        p, buf = O.mixture_solve_z(Z, yv, p, None, lr_p, 1, 16)   # one pass: its cost decides the sample
+        t_pass = time.perf_counter() - a
+        passes = 1
+        while passes < R and (passes + 1) * t_pass <= left:
+            p, buf = O.mixture_solve_z(Z, yv, p, buf, lr_p, 1, 16)
+            passes += 1
+        t_solve = (time.perf_counter() - a) / passes * R
+        a = time.perf_counter()
+        O.aggregate(Ws, p)
+        O.test_eval(Xt, yt, Ws[-1])
+        t_rest = time.perf_counter() - a
+        torch.set_rng_state(state)
+        t_round = t_train + t_z + t_solve + t_rest
+        threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
+        whole = passes == R
+        out['cpu_baseline'] = {
+            'value': N / t_round, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
+            'measured': whole, 'extrapolation_factor': 1.0 if whole else R / passes,
+            'sample': '1 round of the numpy oracle: the chained training of the %d clients (%.2f s), the Z GEMM '
+                      '(%.2f s), %d of the %d p-SGD passes over the %d validation rows (%d steps each; %.2f s per '
+                      'pass%s), aggregate + %d-row test eval' % (
+                          N, t_train, t_z, passes, R, nv, spp, t_pass,
+                          '' if whole else ', scaled to %d passes' % R, len(yt))}
+    return out
+
+
 def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuffle=False, custom=False,
                  fedamw_leg_rounds=0):
     """One BASELINE workload: set up (untimed), ``warmup`` rounds, ``steps`` timed rounds
@@ -587,6 +688,14 @@ def worker(args):
             if rank == 0:
                 print('bench: config %d leg %.1f s, %.0f client-rounds/s' % (cfg, obj['leg_wall_s'], obj['value']),
                       file=sys.stderr, flush=True)
+    if headline and not args.no_legs and ws == 1:
+        t0 = time.perf_counter()
+        obj = config1_leg(dev, cpu_budget=0.0 if args.no_cpu_baseline else args.leg_cpu_seconds)
+        obj['leg_wall_s'] = time.perf_counter() - t0
+        out['config1'] = obj
+        print('bench: config 1 leg %.1f s, %.2f client-rounds/s (%.1f ms per round, p-solve %.3f us per step, %s)'
+              % (obj['leg_wall_s'], obj['value'], obj['ms_per_round'], obj['p_solve_us_per_step'] or float('nan'),
+                 obj['p_solver']), file=sys.stderr, flush=True)
     if rank == 0:
         print(json.dumps(out), file=line_out, flush=True)
     if ws > 1:

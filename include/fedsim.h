@@ -222,7 +222,7 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              teams of 4 that train two clients at once with team-local barriers, so one
  *              team's hand-off and softmax run beside the other team's MFMAs (the split
  *              arithmetic with 4 waves per slice: within the fp32 tolerance of the split form).
- *              G | FS_G_PIPE (ABI 14, ld == 1024 G with G = 2, 4 or 8, 16 < B <= 32, C <= 16, no
+ *              G | FS_G_PIPE (ABI 14, ld == 1024 G with G = 2, 4, 8 or 16, 16 < B <= 32, C <= 16, no
  *              prox term; parallel or chained clients): the "pipe" form -- the split form with
  *              each step's hand-off pipelined by 16-row tile (one tile's partner round trip under
  *              the other tile's forward or backward MFMAs, the softmax per wave in registers, two
@@ -326,6 +326,10 @@ int fs_mix_solve_blocked_covers(int N, int C, int n_val, int epochs, int Bv);
  * with C <= 10; Bv <= 16), _QMC (9, multi-CU quarter-wave), _BIN (10, one wave, two classes:
  * N <= 16, C <= 2, Bv <= 16); 0 = none yet. */
 int fs_mix_solve_last_mode(void);
+/* (ABI 14) Diagnostic: the layout of the calling thread's last fs_mix_solve /
+ * fs_mix_solve_blocked launch when it ran the qmc solver -- its workgroups K and clients per
+ * lane (4 or 8; K = ceil(ldN / (16 * lane_clients))) -- else 0 and 0. */
+int fs_mix_solve_last_layout(int* workgroups, int* lane_clients);
 
 /* ------------------------------------------------------------------------- *
  * Random Fourier feature map.  Replaces RFF's use in feature_mapping

@@ -49,6 +49,7 @@ _SIGS = {
                                        C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_mix_solve_blocked_covers': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     'fs_mix_solve_last_mode': (C.c_int, []),
+    'fs_mix_solve_last_layout': (C.c_int, [C.c_void_p, C.c_void_p]),
     'fs_feature_map': (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                  C.c_float, C.c_void_p, C.c_int64, C.c_void_p]),
     'fs_gram': (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]),
@@ -144,6 +145,13 @@ def get_tuning():
     t = Tuning()
     check(lib().fs_get_tuning(C.byref(t)), 'fs_get_tuning')
     return {k: getattr(t, k) for k, _ in Tuning._fields_}
+
+
+def last_mix_layout():
+    """(workgroups, clients per lane) of the calling thread's last qmc p-solve, else (0, 0)."""
+    k, nk = C.c_int(0), C.c_int(0)
+    check(lib().fs_mix_solve_last_layout(C.byref(k), C.byref(nk)), 'fs_mix_solve_last_layout')
+    return k.value, nk.value
 
 
 def get_process_tuning():

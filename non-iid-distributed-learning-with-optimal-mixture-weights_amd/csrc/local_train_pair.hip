@@ -147,7 +147,7 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     ws[q] = cl ? ld4(start + wbase + 16 * q) : zero4;
-    s0 += ws[q].x * ws[q].x + ws[q].y * ws[q].y + ws[q].z * ws[q].z + ws[q].w * ws[q].w;
+    s0 = sq4_acc(s0, ws[q].x, ws[q].y, ws[q].z, ws[q].w);
   }
   const float nw0 = wave_sum_dpp(s0, lane);      // ||W_start||^2 partial of this wave
   float4 wr[2][4];
@@ -504,14 +504,11 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
           for (int e4 = 0; e4 < 4; ++e4) {
             const float wc = comp(wr[YL][q], e4);
             const float ac = PROX ? comp(ws[q], e4) : 0.f;
-            float gr = ga[e4][q];
-            if (PROX) gr = gr + (wc - ac) * sp;
-            if (P.reg) gr = gr + wc * sr;
-            o[e4] = wc - lr * gr;
+            o[e4] = sgd_w(wc, ga[e4][q], lr, PROX, ac, sp, P.reg, sr);
             if (PROX) {                            // (without a prox term: below, if ridge)
               const float dp = o[e4] - ac;
-              npn += dp * dp;
-              nwn += o[e4] * o[e4];
+              npn = sq_acc(npn, dp);
+              nwn = sq_acc(nwn, o[e4]);
             }
           }
           wr[YL][q] = make_float4(o[0], o[1], o[2], o[3]);
@@ -523,7 +520,7 @@ __global__ __launch_bounds__(PR_THREADS, 1) void local_train_pair_kernel(LTParam
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) nwn += comp(wr[YL][q], e4) * comp(wr[YL][q], e4);
+          for (int e4 = 0; e4 < 4; ++e4) nwn = sq_acc(nwn, comp(wr[YL][q], e4));
       }
       if (PROX || P.reg) {
         npn = PROX ? wave_sum_dpp(npn, lane) : 0.f;

@@ -75,6 +75,23 @@ __device__ __forceinline__ void pp_own(T& x) {
   asm volatile("; pr-own %0" : "+v"(x));
 }
 
+// Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup
+#ifdef FS_STAMPS
+#define PP_STAMP(k)                                                                       \
+  {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long t_;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (k > 0) stamp_acc[k > 0 ? k - 1 : 0] += t_ - stamp_prev;                           \
+    stamp_prev = t_;                                                                      \
+  }
+#else
+#define PP_STAMP(k)
+#endif
+
+__device__ __forceinline__ float invb_of(int bc) { return 1.0f / (float)bc; }
+
 template <int G, bool NRM>
 __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParams P, SplitWS X) {
   constexpr int NW = PP_WAVES, TPW = PP_TPW, RS = PP_RS, NC = 16;
@@ -82,7 +99,13 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   // wave partial logits, transposed: zpt[w][rt][class * ZS + 4 lg + kk] = the partial of row
   // 16 rt + 4 kk + lg -- one ds_read_b128 per wave gives a lane its four rows of the tile
   __shared__ __attribute__((aligned(16))) float zpt[NW][2][NC * PP_ZS];
-  __shared__ int labw[NW][2][PP_NR];       // wave-private copies of the step's labels (by parity)
+  // softmax gradients of the step (by parity): gsm[par][rt][lane][kk] = g of (row 16 rt + 4 kk + lg,
+  // class l16), written by wave 4 rt + kk, read back by every wave as one ds_read_b128; the
+  // flags gfl[par][rt][kk] carry the step's tag once wave 4 rt + kk has written its column
+  __shared__ __attribute__((aligned(16))) float gsm[2][2][64][4];
+  __shared__ __attribute__((aligned(16))) unsigned gfl[2][2][4];
+  __shared__ float cesm[2][8];             // per 4-row group CE wave sums (the reported loss)
+  __shared__ float wn2sm[2];               // ||W||^2 at the step's start (ridge), by wave 0
   __shared__ float wred[NW][2];            // ||W - W_a||^2 (always 0 here), ||W||^2 of the wave's slice
   extern __shared__ __attribute__((aligned(16))) float xs_dyn[];   // [32][RS] batch slice image
 
@@ -130,8 +153,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (l16 >= C) wr[i][q] = zero4;
-        s += wr[i][q][0] * wr[i][q][0] + wr[i][q][1] * wr[i][q][1] + wr[i][q][2] * wr[i][q][2] +
-             wr[i][q][3] * wr[i][q][3];
+        s = sq4_acc(s, wr[i][q][0], wr[i][q][1], wr[i][q][2], wr[i][q][3]);
       }
     return wave_sum_dpp(s, lane);
   };
@@ -222,6 +244,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
       for (int q = 0; q < 4; ++q) pp_own(xf[i][rt][q]);
   }
   take_rows();
+  if (tid < 16) (&gfl[0][0][0])[tid] = 0u;       // (tag 0 is never a step's tag)
   lds_barrier();
 
   auto flush_empty = [&](int ka, int kb) {
@@ -246,17 +269,24 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     }
   };
 
-  // Per step every wave issues, in this order (counted vector-memory operations):
+  // Per step, wave w publishes and polls like every other, but computes the softmax of ONE
+  // 16-lane-row column: row tile h = w / 4, rows 4 kk + lg with kk = w % 4 -- 64 of the tile's
+  // 256 (row, class) entries, as the split form spreads its softmax over its 8 waves -- and
+  // hands the g values to the other waves through LDS (gsm + a tag flag per column, no
+  // barrier): waves 0-3 finish tile 0's softmax while waves 4-7 still wait for tile 1's
+  // partners, so a SIMD's two waves (one of each half) overlap one's round trip with the
+  // other's backward MFMAs.  Every wave issues, in this order (counted vector-memory ops):
   //   [client start: 8 weight loads, drained at once]  1 publish store (rt0)  NRM norm store
-  //   1 publish store (rt1)  P0 polls (rt0: 4 (G-1) + NRM (G-1))  2 label loads  8 row loads (next
-  //   step, rt0)  P1 polls (rt1: 4 (G-1))  8 row loads (next step, rt1)  2 index loads
-  // -- so at the forward of rt0 its rows (issued one step ago) have P1 + 8 + 2 operations behind
-  // them, the rows of rt1 2 + 1 + NRM, the indices 1 + NRM + 1 + P0, the rt0 polls 2 + 8, the
-  // rt1 polls 8.  A re-poll drains everything (vmcnt(0)); other extra operations (client-end
-  // stores, spills) only make a wait stricter.
-  constexpr int P0 = 4 * (G - 1) + (NRM ? G - 1 : 0), P1 = 4 * (G - 1);
-  constexpr int W_F0 = P1 + 8 + 2, W_F1 = 2 + 1 + (NRM ? 1 : 0), W_IDX = 1 + (NRM ? 1 : 0) + 1 + P0;
-  constexpr int W_POLL0 = 2 + 8, W_POLL1 = 8;
+  //   1 publish store (rt1)  [wait: the indices]  PH polls (its column: G - 1; wave 0 also the
+  //   norms: G - 1)  [wait 0: every poll lands before any row is issued]  2 label loads
+  //   8 row loads (next step, rt0: one per backward iteration of K0)  8 row loads (rt1, in K1)
+  //   2 index loads
+  // -- so at the forward of rt0 its rows (one step ago) have 8 + 2 operations behind them, the
+  // rows of rt1 2 + 1 + NRM, the indices 1 + NRM + 1.  A stale poll is re-polled with nothing
+  // else in flight.  Other extra operations (client-end stores, spills) only make a wait
+  // stricter.
+  constexpr int W_F0 = 8 + 2, W_F1 = 2 + 1 + (NRM ? 1 : 0), W_IDX = 1 + (NRM ? 1 : 0) + 1;
+  const int hrt = w >> 2, kcol = w & 3;          // this wave's softmax column: row tile, kk
 
   SpCur cc;
   bool cc_ok = sp_seek<true>(cc, P, grp, ng, T, 0);
@@ -265,9 +295,13 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   bool dead = false;
   double lsum = 0.0;
   const int rblk = 4 * (l16 & 3) + (l16 >> 2);
-  unsigned long long pl[4][GP];
+  unsigned long long pl[GP];
   unsigned long long pnrm[GP];
+#ifdef FS_STAMPS
+  unsigned long long stamp_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
+#endif
   for (; cc_ok; ++gs) {
+    PP_STAMP(0)
     const int st = cc.st, n = cc.n, nbat = cc.nbat;
     if (st == 0) {
       if (!P.chained && gs > 0) {
@@ -284,6 +318,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     const unsigned tag32 = X.tag_base + gs + 1u;
     const unsigned long long tag = (unsigned long long)tag32 << 32;
     unsigned long long* slot = xb + (int64_t)par * G * PP_SZ;
+    const bool need_ce = g == 0 && e == E - 1;     // the cross-entropy feeds only the reported loss
 
     // ---- forward of one row tile; its wave partial goes to LDS transposed ----
     auto forward = [&](int rt) {
@@ -312,118 +347,24 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     };
     // (waves w and w + 4 publish the same component kk = w & 3: one unconditional store each)
     auto publish = [&](int rt, const floatx4& v) {
-      const int kk = w & 3;
-      const float x = kk == 0 ? v[0] : (kk == 1 ? v[1] : (kk == 2 ? v[2] : v[3]));
-      __hip_atomic_store(slot + (int64_t)g * PP_SZ + rt * 256 + kk * 64 + lane, tag | __float_as_uint(x),
+      const float x = kcol == 0 ? v[0] : (kcol == 1 ? v[1] : (kcol == 2 ? v[2] : v[3]));
+      __hip_atomic_store(slot + (int64_t)g * PP_SZ + rt * 256 + kcol * 64 + lane, tag | __float_as_uint(x),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // ---- polls: the G - 1 partners' granules of this lane's four rows of a tile ----
-    auto poll = [&](int rt) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int k = 0; k < G - 1; ++k) {
-          const int h = k + (k >= g ? 1 : 0);
-          pp_poll(pl[kk][k], slot + (int64_t)h * PP_SZ + rt * 256 + kk * 64 + lane);
-        }
-      if (NRM && rt == 0)
-#pragma unroll
-        for (int k = 0; k < G - 1; ++k) {
-          const int h = k + (k >= g ? 1 : 0);
-          pp_poll(pnrm[k], slot + (int64_t)h * PP_SZ + 512 + (lane & 1));
-        }
-    };
-    auto own_polls = [&](int rt) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int k = 0; k < G - 1; ++k) pp_own(pl[kk][k]);
-      if (NRM && rt == 0)
-#pragma unroll
-        for (int k = 0; k < G - 1; ++k) pp_own(pnrm[k]);
-    };
-    unsigned spins = 0;
-    // (call after the counted wait and the own statements of the first poll; a stale partner
-    // re-polls everything and drains the queue)
-    auto wait_poll = [&](int rt) {
-      if (X.spin_limit == 0 && gs == 0 && lane == 0)      // test knob: report an injected timeout
-        __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (;;) {
-        bool ok = true;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-          for (int k = 0; k < G - 1; ++k) ok &= (l16 >= C) | ((unsigned)(pl[kk][k] >> 32) == tag32);
-        if (NRM && rt == 0)
-#pragma unroll
-          for (int k = 0; k < G - 1; ++k) ok &= (unsigned)(pnrm[k] >> 32) == tag32;
-        if (__all(ok)) break;
-        if (dead || ++spins > X.spin_limit) {
-          if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          dead = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        poll(rt);
-        pp_wait<0>();
-        own_polls(rt);
-      }
-    };
-    // the slice-order sum (own partial at position g): every partner gets the same bits
-    auto slice_sum = [&](float own, int kk) {
-      float sum = 0.f;
-#pragma unroll
-      for (int h = 0; h < G; ++h) {
-        float pv = 0.f;
-#pragma unroll
-        for (int k = 0; k < G - 1; ++k)
-          if (k + (k >= g ? 1 : 0) == h) pv = __uint_as_float((unsigned)pl[kk][k]);
-        sum += (h == g) ? own : pv;
-      }
-      return sum;
-    };
-    // ---- softmax of one tile in the backward's operand layout ----
-    const float invb = 1.0f / (float)bc;
-    float gB[8], cep[8];
-    auto softmax = [&](int rt, const floatx4& own) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int r = 16 * rt + 4 * kk + lg;
-        const float z0 = slice_sum(own[kk], kk);
-        const bool valid = r < bc && l16 < C;
-        const float z = valid ? z0 : 0.f;
-        float m = valid ? z : -INFINITY;
-#pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
-        const float ex = valid ? __expf(z - m) : 0.f;
-        float se = ex;
-#pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
-        float gv = 0.f, ce = 0.f;
-        if (valid) {
-          const bool isy = l16 == labw[w][par][r];
-          gv = (isy ? -invb : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb;
-          if (isy) ce -= z - m - __logf(se);
-        }
-        gB[4 * rt + kk] = gv;
-        cep[4 * rt + kk] = ce;
-      }
     };
 
     // ================= row tile 0: forward, publish =================
     pp_wait<W_F0>();                                // this step's rt0 rows and labels landed
+    PP_STAMP(1)
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) pp_own(lb[rt]);
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) pp_own(xf[i][0][q]);
-    if (lg == 0) {
-      labw[w][par][l16] = lb[0];
-      labw[w][par][16 + l16] = lb[1];
-    }
     forward(0);
+    PP_STAMP(2)
     lds_barrier();                                  // B1a: wave partials of rt0 (and the norms)
+    PP_STAMP(3)
     const floatx4 own0 = own_sum(0);
     float nown[2] = {0.f, 0.f};
     if (NRM) {
@@ -435,20 +376,39 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
       __hip_atomic_store(slot + (int64_t)g * PP_SZ + 512 + lane, tag | __float_as_uint(nown[lane & 1]),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ================= row tile 1: forward (rt0's round trip runs under it), publish ========
+    PP_STAMP(4)
     pp_wait<W_F1>();                                // this step's rt1 rows landed
+    PP_STAMP(5)
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) pp_own(xf[i][1][q]);
     forward(1);
+    PP_STAMP(6)
     lds_barrier();                                  // B1b
+    PP_STAMP(7)
     const floatx4 own1 = own_sum(1);
     publish(1, own1);
-    poll(0);
     pp_wait<W_IDX>();                               // the next step's row indices landed
     take_rows();
-    // image of this wave's tiles for the backward (wave-private: no barrier); then the next
-    // step's labels and row-tile-0 rows stream from here on, behind the polls
+    // ---- this wave's column of the softmax: the partners' granules of (row tile hrt, kk) ----
+    const bool nrm_w = NRM && w == 0;               // wave 0 also polls the norms
+    auto poll = [&]() {
+#pragma unroll
+      for (int k = 0; k < G - 1; ++k) {
+        const int h = k + (k >= g ? 1 : 0);
+        pp_poll(pl[k], slot + (int64_t)h * PP_SZ + hrt * 256 + kcol * 64 + lane);
+      }
+      if (nrm_w)
+#pragma unroll
+        for (int k = 0; k < G - 1; ++k) {
+          const int h = k + (k >= g ? 1 : 0);
+          pp_poll(pnrm[k], slot + (int64_t)h * PP_SZ + 512 + (lane & 1));
+        }
+    };
+    poll();
+    PP_STAMP(8)
+    // image of this wave's tiles for the backward (wave-private: no barrier), under the round trip
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
@@ -457,29 +417,118 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
         for (int q = 0; q < 4; ++q)
           st4(xs_dyn + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg),
               make_float4(xf[i][rt][q][0], xf[i][rt][q][1], xf[i][rt][q][2], xf[i][rt][q][3]));
-    // (the image has read xf before the loads below refill it)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    issue_labels();
-    issue_rows(0);
-    pp_wait<W_POLL0>();
-    own_polls(0);
-    wait_poll(0);
-    float wn2 = 0.f;
-    if (NRM) {
-      // ||W||^2 at the start of this step: slice-order sum (lane 1; lane 0 holds ||W - W_a||^2)
-      float ns = 0.f;
-      const float mine = (lane & 1) ? nown[1] : nown[0];
+    PP_STAMP(9)
+    pp_wait<0>();
+#pragma unroll
+    for (int k = 0; k < G - 1; ++k) pp_own(pl[k]);
+    if (nrm_w)
+#pragma unroll
+      for (int k = 0; k < G - 1; ++k) pp_own(pnrm[k]);
+    {
+      if (X.spin_limit == 0 && gs == 0 && lane == 0)      // test knob: report an injected timeout
+        __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < G - 1; ++k) ok &= (l16 >= C) | ((unsigned)(pl[k] >> 32) == tag32);
+        if (nrm_w)
+#pragma unroll
+          for (int k = 0; k < G - 1; ++k) ok &= (unsigned)(pnrm[k] >> 32) == tag32;
+        if (__all(ok)) break;
+        if (dead || ++spins > X.spin_limit) {
+          if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        poll();
+        pp_wait<0>();
+#pragma unroll
+        for (int k = 0; k < G - 1; ++k) pp_own(pl[k]);
+        if (nrm_w)
+#pragma unroll
+          for (int k = 0; k < G - 1; ++k) pp_own(pnrm[k]);
+      }
+    }
+    PP_STAMP(10)
+    {
+      // slice-order sum (own partial at position g): every partner gets the same bits
+      const floatx4& own = hrt ? own1 : own0;
+      const float ownv = kcol == 0 ? own[0] : (kcol == 1 ? own[1] : (kcol == 2 ? own[2] : own[3]));
+      float z0 = 0.f;
 #pragma unroll
       for (int h = 0; h < G; ++h) {
         float pv = 0.f;
 #pragma unroll
         for (int k = 0; k < G - 1; ++k)
-          if (k + (k >= g ? 1 : 0) == h) pv = __uint_as_float((unsigned)pnrm[k]);
-        ns += (h == g) ? mine : pv;
+          if (k + (k >= g ? 1 : 0) == h) pv = __uint_as_float((unsigned)pl[k]);
+        z0 += (h == g) ? ownv : pv;
       }
-      wn2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ns), 1));
+      if (nrm_w) {
+        // ||W||^2 at the start of this step: slice-order sum (lane 1; lane 0: ||W - W_a||^2)
+        float ns = 0.f;
+        const float mine = (lane & 1) ? nown[1] : nown[0];
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          float pv = 0.f;
+#pragma unroll
+          for (int k = 0; k < G - 1; ++k)
+            if (k + (k >= g ? 1 : 0) == h) pv = __uint_as_float((unsigned)pnrm[k]);
+          ns += (h == g) ? mine : pv;
+        }
+        if (lane == 1) wn2sm[par] = ns;
+      }
+      // the softmax of (row 16 hrt + 4 kcol + lg, class l16) -- the split form's arithmetic: its
+      // xor butterflies 8, 4, 2, 1 over the class lanes with the same bits (the max is exact in
+      // any order: four DPP rotations; in the sum, after the xor-8 level every lane's row_ror:4
+      // partner holds the xor-4 partner's value)
+      const int r = 16 * hrt + 4 * kcol + lg;
+      const bool valid = r < bc && l16 < C;
+      const float z = valid ? z0 : 0.f;
+      const float m = row16_all<true>(valid ? z : -INFINITY);
+      const float ex = valid ? __expf(z - m) : 0.f;
+      float se = ex + dpp<0x128>(ex);                       // row_ror:8 = xor 8
+      se = se + dpp<0x124>(se);                             // row_ror:4 (= the xor-4 value here)
+      se = se + dpp<0x4E>(se);                              // quad xor 2
+      se = se + dpp<0xB1>(se);                              // quad xor 1
+      const int lab = __shfl(hrt ? lb[1] : lb[0], 4 * kcol + lg, 64);   // label of row r
+      float gv = 0.f, ce = 0.f;
+      if (valid) {
+        const bool isy = l16 == lab;
+        gv = (isy ? -invb_of(bc) : 0.f) + ex * __builtin_amdgcn_rcpf(se) * invb_of(bc);
+        if (need_ce && isy) ce -= z - m - __logf(se);
+      }
+      gsm[par][hrt][lane][kcol] = gv;
+      if (need_ce) {
+        ce = wave_sum_dpp(ce, lane);              // the split form's wave (4 hrt + kcol) CE sum
+        if (lane == 0) cesm[par][w] = ce;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the column (and wn2) before its flag
+      if (lane == 0) gfl[par][hrt][kcol] = tag32;
     }
-    softmax(0, own0);
+    // the next step's labels (the polls have all landed and this step's labels are read: nothing
+    // of ours waits behind them)
+    issue_labels();
+    PP_STAMP(11)
+    // ---- the g values of a row tile, once its four columns are flagged ----
+    float gB[8];
+    auto take_g = [&](int rt) {
+      unsigned sp = 0;
+      for (;;) {
+        typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+        const uintx4 f = *reinterpret_cast<volatile const uintx4*>(&gfl[par][rt][0]);
+        if ((f[0] == tag32) & (f[1] == tag32) & (f[2] == tag32) & (f[3] == tag32)) break;
+        if (dead || ++sp > 64u * X.spin_limit) {
+          if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const floatx4 v = *reinterpret_cast<volatile const floatx4*>(&gsm[par][rt][lane][0]);
+      gB[4 * rt + 0] = v[0]; gB[4 * rt + 1] = v[1]; gB[4 * rt + 2] = v[2]; gB[4 * rt + 3] = v[3];
+    };
 
     // ================= backward: image rows 4 kk + lg, kk = 0..7 =================
     floatx4 ga[TPW][4];
@@ -487,7 +536,10 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) ga[i][e4] = zero4;
-    auto bwd = [&](int kk0) {
+    // (with the next step's 8 row loads of tile-row rt_ld, one per (tile, kk) iteration: the
+    // stream spreads over the phase's MFMAs instead of a burst that fills the memory queue)
+    auto bwd = [&](int kk0, int rt_ld) {
+      const float* src = P.phi + (int64_t)pn[rt_ld] * ld + 64 * t0 + 4 * lg + 64 * w;
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         const int Tl = w + NW * i;
@@ -498,29 +550,39 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
           const float4 x = ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RS);
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) ga[i][e4] = mfma4(comp(x, e4), gB[kk], ga[i][e4]);
+          const int f = 4 * i + (kk - kk0);          // row piece (tile f / 4, q = f % 4)
+          switch (f) {
+            case 0: pp_ld4<0>(xf[0][rt_ld][0], src); break;
+            case 1: pp_ld4<64>(xf[0][rt_ld][1], src); break;
+            case 2: pp_ld4<128>(xf[0][rt_ld][2], src); break;
+            case 3: pp_ld4<192>(xf[0][rt_ld][3], src); break;
+            case 4: pp_ld4<2048>(xf[1][rt_ld][0], src); break;
+            case 5: pp_ld4<2112>(xf[1][rt_ld][1], src); break;
+            case 6: pp_ld4<2176>(xf[1][rt_ld][2], src); break;
+            default: pp_ld4<2240>(xf[1][rt_ld][3], src); break;
+          }
         }
       }
     };
-    bwd(0);                                         // K0 (rt1's round trip runs under it)
-    poll(1);
-    issue_rows(1);
-    pp_wait<W_POLL1>();
-    own_polls(1);
-    wait_poll(1);
-    softmax(1, own1);
-    if (g == 0 && w == 0 && e == E - 1) {
-      // the loss as the split form sums it: per 4-row group (split wave 4 rt + kk) a DPP wave
-      // sum, then the eight in row order
+    take_g(0);
+    PP_STAMP(12)
+    bwd(0, 0);                                      // K0 (beside the other half's round trip)
+    PP_STAMP(13)
+    take_g(1);
+    float wn2 = 0.f;
+    if (NRM) wn2 = wn2sm[par];
+    if (need_ce && w == 0) {
+      // the loss as the split form sums it: the eight 4-row-group CE sums in row order
       float ce = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) ce += wave_sum_dpp(cep[k], lane);
+      for (int k = 0; k < 8; ++k) ce += cesm[par][k];
       if (lane == 0) {
         float loss = ce / (float)bc;
         if (P.reg) loss = loss + P.lam * sqrtf(wn2);
         lsum += (double)loss * (double)bc;
       }
     }
-    bwd(4);                                         // K1
+    bwd(4, 1);                                      // K1
     // ---- update of the register-resident slice ----
     {
       const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
@@ -531,12 +593,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
 #pragma unroll
           for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) {
-              const float wc = wr[i][q][e4];
-              float gr = ga[i][e4][q];
-              if (P.reg) gr = gr + wc * sr;
-              wr[i][q][e4] = wc - lr * gr;
-            }
+            for (int e4 = 0; e4 < 4; ++e4) wr[i][q][e4] = sgd_w(wr[i][q][e4], ga[i][e4][q], lr, false, 0.f, 0.f, P.reg, sr);
       }
     }
     if (NRM) {
@@ -547,7 +604,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) nwn += wr[i][q][e4] * wr[i][q][e4];
+          for (int e4 = 0; e4 < 4; ++e4) nwn = sq_acc(nwn, wr[i][q][e4]);
       nwn = wave_sum_dpp(nwn, lane);
       if (lane == 0) { wred[w][0] = 0.f; wred[w][1] = nwn; }
     }
@@ -560,13 +617,20 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     const int kprev = cc.k;
     cc_ok = sp_advance<true>(cc, P, grp, ng, T);
     flush_empty(kprev + 1, cc_ok ? cc.k : T);
+    PP_STAMP(14)
   }
   pp_wait<0>();                                     // nothing of ours is in flight at the exit
+#ifdef FS_STAMPS
+  // (every wave: [grid][8 waves][16])
+  if (lane == 0 && X.stamps) {
+    for (int k = 0; k < 14; ++k) X.stamps[(blockIdx.x * 8 + w) * 16 + k] = stamp_acc[k];
+    X.stamps[(blockIdx.x * 8 + w) * 16 + 15] = (unsigned long long)gs;
+  }
+#endif
 }
 
 bool pipe_fits(int C, int B, int NT, int G, int prox) {
-  // (G = 8 holds 4 x 7 polled granules per lane: ~200 VGPRs spilled; G = 16 more -- not built)
-  if (!(G == 2 || G == 4)) return false;
+  if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
   return !prox && C >= 1 && C <= 16 && B > 16 && B <= 32 && NT == PP_NTS * G;
 }
 
@@ -596,7 +660,7 @@ unsigned split_spin_bound();   // local_train_split.hip: fs_tuning.spin_limit / 
 int launch_local_train_pipe(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
   const int NT = (int)(P.ld >> 6);
   if (!pipe_fits(P.C, P.B, NT, G, P.prox))
-    return fail(FS_EUNSUPPORTED, "fs_local_train: the pipe form needs ld = 1024 G (G = 2 or 4), 16 < B <= 32, "
+    return fail(FS_EUNSUPPORTED, "fs_local_train: the pipe form needs ld = 1024 G (G = 2, 4, 8 or 16), 16 < B <= 32, "
                                  "C <= 16 and no prox term");
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
@@ -613,6 +677,9 @@ int launch_local_train_pipe(const LTParams& P, int G, void* ws, int64_t ws_bytes
   X.spin_limit = split_spin_bound();
   X.poll_delay = 0;
   X.stamps = nullptr;
+#ifdef FS_STAMPS
+  X.stamps = reinterpret_cast<unsigned long long*>(base + xbytes);
+#endif
   // hand-off tags by launch generation (as the split form, local_train_split.hip)
   const int64_t groups_clients = P.chained ? P.N : (P.N + ng - 1) / ng;
   const bool long_launch = P.max_client_steps <= 0 || P.max_client_steps * groups_clients >= (1 << 20) - 1;
@@ -629,7 +696,8 @@ int launch_local_train_pipe(const LTParams& P, int G, void* ws, int64_t ws_bytes
   switch (G) {
     case 2: launch_pipe_g<2>(P, X, grid, lds, st); break;
     case 4: launch_pipe_g<4>(P, X, grid, lds, st); break;
-    default: launch_pipe_g<4>(P, X, grid, lds, st); break;
+    case 8: launch_pipe_g<8>(P, X, grid, lds, st); break;
+    default: launch_pipe_g<16>(P, X, grid, lds, st); break;
   }
   return FS_OK;
 }

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         wr[i][q] = ok ? ld4(start + base + 64 * Tl + 16 * q) : zero4;
-        s += wr[i][q].x * wr[i][q].x + wr[i][q].y * wr[i][q].y + wr[i][q].z * wr[i][q].z + wr[i][q].w * wr[i][q].w;
+        s = sq4_acc(s, wr[i][q].x, wr[i][q].y, wr[i][q].z, wr[i][q].w);
       }
     }
     return wave_sum_dpp(s, lane);
@@ -600,14 +600,11 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
               for (int e4 = 0; e4 < 4; ++e4) {
                 const float wc = comp(wr[i][q], e4);
                 const float ac = PROX ? comp(av[q], e4) : 0.f;
-                float gr = ga[e4][q];
-                if (PROX) gr = gr + (wc - ac) * sp;
-                if (P.reg) gr = gr + wc * sr;
-                o[e4] = wc - lr * gr;
+                o[e4] = sgd_w(wc, ga[e4][q], lr, PROX, ac, sp, P.reg, sr);
                 if (PROX) {                        // (without a prox term: after the loop, if ridge)
                   const float dp = o[e4] - ac;
-                  npn += dp * dp;
-                  nwn += o[e4] * o[e4];
+                  npn = sq_acc(npn, dp);
+                  nwn = sq_acc(nwn, o[e4]);
                 }
               }
               wr[i][q] = make_float4(o[0], o[1], o[2], o[3]);
@@ -643,7 +640,7 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
 #pragma unroll
           for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) nwn += comp(wr[i][q], e4) * comp(wr[i][q], e4);
+            for (int e4 = 0; e4 < 4; ++e4) nwn = sq_acc(nwn, comp(wr[i][q], e4));
       }
       if (PROX || P.reg) {
         npn = PROX ? wave_sum_dpp(npn, lane) : 0.f;
@@ -903,10 +900,16 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
       return FS_OK;
     }
   }
-  // the pipe form by tuning (fs_tuning.split_pipe = 1: wherever it fits; 0 = by shape, -1 = never)
-  if (!(want > 1 && want < FS_G_PAIR) && tuning().split_pipe > 0 && NT % 16 == 0) {
+  // the pipe form (fs_tuning.split_pipe = 1: wherever it fits; -1 = never; 0 = by shape: parallel
+  // clients at G <= 4 where its groups walk several clients each -- config 4, 1,250 clients of 64
+  // rows on 128 groups of 2: 395-409 vs 419-448 us per launch for the pair form (G = 4) and
+  // 285-302 vs 300-310 us at config 2's 100 clients, where the split form stays
+  // (profiles/r05/pipe_vs_forms.txt); config 5's G = 16: 6.5 vs 4.9 ms, not chosen)
+  if (!(want > 1 && want < FS_G_PAIR) && NT % 16 == 0 && tuning().split_pipe >= 0) {
     const int g = NT / 16;
-    if (pipe_fits(C, B, NT, g, prox) && g <= cus) {
+    const bool by_shape = tuning().split_pipe == 0 && want == 0 && tuning().train_form == 0 && !chained &&
+                          g <= 4 && N > pipe_groups(N, g, 0, cus);
+    if ((tuning().split_pipe > 0 || by_shape) && pipe_fits(C, B, NT, g, prox) && g <= cus) {
       *G_out = g | FS_G_PIPE;
       *ws_bytes_out = pipe_ws_bytes(N, g, chained, cus);
       return FS_OK;

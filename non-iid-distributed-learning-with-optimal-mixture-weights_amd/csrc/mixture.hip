@@ -2395,6 +2395,10 @@ static bool qmc_covers(int N, int C, int Bv, int nv, int epochs) {
          zb < ((int64_t)1 << 31) && (int64_t)epochs * nv < ((int64_t)1 << 31);
 }
 
+// the calling thread's last multi-CU launch layout (fs_mix_solve_last_layout): workgroups K and
+// clients per lane NK of the qmc solver (0, 0 after any other solver)
+static thread_local int t_last_k = 0, t_last_nk = 0;
+
 // 1: not covered; 0: launched; < 0: error
 static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const int32_t* perms, int N, int C, int nv,
                          int epochs, int Bv, float lr, float mom, float* p, float* buf, int* first, void* d_ws,
@@ -2415,6 +2419,8 @@ static int mix_solve_qmc(hipStream_t st, const float* Z, const int32_t* y, const
   const dim3 grid(MC_XCDS * (K + h)), block(MQ_WAVES * 64);
   const int zb = (int)((int64_t)nv * C * mix_ldn(N) * 4);
   const int pd = qmc_poll_delay(K, C);
+  t_last_k = K;
+  t_last_nk = nk;
   if (nk == 8)
     hipLaunchKernelGGL((mix_solve_qmc_kernel<8, 10, 2, quad_split<10>()>), grid, block, 0, st, Z, y, perms, N, C, nv,
                        epochs, Bv, lr, mom, p, buf, first, zb, ws, err, K, spin_limit, pf.prog, h, pf.lead, zL, zR,
@@ -2437,6 +2443,14 @@ using namespace fs;
 static thread_local int t_last_solver = 0;
 
 extern "C" int fs_mix_solve_last_mode(void) { return t_last_solver; }
+
+extern "C" int fs_mix_solve_last_layout(int* workgroups, int* lane_clients) {
+  FS_REQUIRE(workgroups && lane_clients, "null pointer");
+  const bool q = t_last_solver == FS_SOLVER_QMC;
+  *workgroups = q ? fs::t_last_k : 0;
+  *lane_clients = q ? fs::t_last_nk : 0;
+  return FS_OK;
+}
 
 extern "C" int64_t fs_mix_solve_ws_bytes(int N, int C, int Bv) {
   if (N < 1) return MC_ERR_BYTES;

@@ -38,6 +38,25 @@ struct SplitWS {
 
 __device__ __forceinline__ int tile_lo(int g, int G, int NT) { return (int)(((int64_t)NT * g) / G); }
 
+// The weight update and the squared norms with every rounding spelled out (explicit fma, no
+// contraction left to the compiler, which fused `a*a + b*b` as fma(b, b, a*a) in one kernel and
+// fma(a, a, b*b) in another): the split, pair and pipe forms share these, so they agree
+// bitwise by construction.  s + (x^2 + y^2 + z^2 + w^2), the four as one fma chain from x^2:
+__device__ __forceinline__ float sq4_acc(float s, float x, float y, float z, float w) {
+  float t = x * x;
+  t = __builtin_fmaf(y, y, t);
+  t = __builtin_fmaf(z, z, t);
+  t = __builtin_fmaf(w, w, t);
+  return s + t;
+}
+__device__ __forceinline__ float sq_acc(float s, float x) { return __builtin_fmaf(x, x, s); }
+// w - lr * (g + [prox] (w - a) sp + [reg] w sr)
+__device__ __forceinline__ float sgd_w(float wc, float g, float lr, bool prox, float ac, float sp, bool reg, float sr) {
+  if (prox) g = __builtin_fmaf(wc - ac, sp, g);
+  if (reg) g = __builtin_fmaf(wc, sr, g);
+  return __builtin_fmaf(-lr, g, wc);
+}
+
 // LDS image of one step's batch slice: row-major, row stride RS = DS + 8 floats, and the
 // sixteen float4 blocks of every 64-column tile permuted by block ^ (row & 7).  With this
 // layout both the image write (lanes 0-7 = eight rows, same block) and the backward's read

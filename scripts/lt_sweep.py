@@ -36,6 +36,7 @@ def main():
     ap.add_argument('--chained', action='store_true')
     ap.add_argument('--prox', action='store_true')
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--reg', type=int, default=1, help='ridge term on (FedAMW local training) or off (FedAvg)')
     a = ap.parse_args()
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
@@ -57,13 +58,13 @@ def main():
         W0 = torch.zeros(C, feats.ld, device=dev)
         W0.normal_(0, 0.01)
         for _ in range(2):
-            tr.run(W0, 0.5, a.prox, 1e-3, True, 1e-5, chained)
+            tr.run(W0, 0.5, a.prox, 1e-3, bool(a.reg), 1e-5, chained)
         torch.cuda.synchronize()
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            tr.run(W0, 0.5, a.prox, 1e-3, True, 1e-5, chained)
+            tr.run(W0, 0.5, a.prox, 1e-3, bool(a.reg), 1e-5, chained)
             e1.record()
             ts.append((e0, e1))
         torch.cuda.synchronize()

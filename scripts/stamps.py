@@ -20,6 +20,8 @@ from scripts.lt_sweep import SHAPES  # noqa: E402
 NAMES = ['fwd', 'S1', 'sum+publish', 'poll+sum', 'next(early)', 'S2', 'softmax+S3+next', 'bwd+update']
 PAIR_NAMES = ['wait rows', 'fwd', 'S1', 'publish+img', 'wait polls', 'check', 'sum+S2', 'softmax+S3',
               'issue', 'bwd+update']
+PIPE_NAMES = ['wait rows0', 'fwd0', 'B1a', 'own0+pub0', 'wait rows1', 'fwd1', 'B1b', 'own1+pub1+poll0+idx',
+              'img', 'wait poll0', 'smax0+poll1+issue0', 'K0', 'wait poll1+issue1', 'smax1+K1+upd+end']
 
 
 def main():
@@ -29,6 +31,7 @@ def main():
     ap.add_argument('--chained', action='store_true')
     ap.add_argument('--pair', action='store_true', help='the pair form at width --G (or the planner\'s)')
     ap.add_argument('--teams', action='store_true', help='the team form at width --G (team 0 stamped)')
+    ap.add_argument('--pipe', action='store_true', help='the pipe form at width --G')
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
     sh = SHAPES[a.config]
@@ -37,12 +40,14 @@ def main():
     N, D, C, E, B = sh['clients'], sh['D'], sh['C'], 2, 32
     d = data.federated(N, sh['rows'], D, C, 1000, shape=sh['shape'], device=dev)
     feats = engine.Features(d['X_train'], d['y_train'], D, dev)
-    split = (a.G | fedamw_amd._lib.G_PAIR if a.pair else (a.G | fedamw_amd._lib.G_TEAMS if a.teams else a.G)) or None
+    L = fedamw_amd._lib
+    split = (a.G | L.G_PAIR if a.pair else (a.G | L.G_TEAMS if a.teams else (a.G | L.G_PIPE if a.pipe else a.G))) or None
     tr = engine.LocalTrainer(feats, C, B, E, split=split, chained=chained)
-    names = PAIR_NAMES if tr.pair else NAMES
+    names = PAIR_NAMES if tr.pair else (PIPE_NAMES if tr.pipe else NAMES)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     grid = 8 * tr.width if chained else tr.groups(cus) * tr.width
-    extra = grid * 16 * 8
+    per_wave = 8 if tr.pipe else 1                              # the pipe form stamps every wave
+    extra = grid * per_wave * 16 * 8
     base = tr.ws.numel() - fedamw_amd._lib.ERR_BLOCK          # exchange granules; stamps go right after
     tr.ws = torch.zeros(tr.ws.numel() + extra, dtype=torch.uint8, device=dev)
     torch.manual_seed(0)
@@ -53,6 +58,14 @@ def main():
     torch.cuda.synchronize()
     tr.check_errors()
     st = tr.ws[base:base + extra].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
+    if per_wave > 1:
+        allw = st.reshape(-1, per_wave, 16)
+        allw = allw[allw[:, 0, 15] > 0]
+        pw = allw[:, :, :14] / allw[:, :, 15:16]
+        print('per wave (mean over workgroups), cycles/step:')
+        for k, nm in enumerate(PIPE_NAMES):
+            print('  %-22s' % nm + ' '.join('%6.0f' % pw[:, wv, k].mean() for wv in range(per_wave)))
+        st = allw[:, 0, :]
     st = st[st[:, 15] > 0]
     steps = st[:, 15]
     per = st[:, :len(names)] / steps[:, None]

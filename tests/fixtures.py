@@ -1,5 +1,6 @@
 """Helpers to load the golden fixtures written by tests/golden/make_golden.py."""
 import glob
+import json
 import os
 
 import numpy as np
@@ -68,16 +69,26 @@ LOSS_RTOL = 1e-5
 P_RTOL = 1e-5
 
 
-# The chained 300-client qmc horizon case (make_golden.py HORIZON['qmc'], 6,000 sequential client
-# trainings): the CPU restatement's own distance from the reference grows ~linearly with the
-# rounds (W 4e-7 after round 0, 1.06e-5 at round 18; p 1.4e-5 at round 19 -- the fp32 summation
-# order of 20 rounds x 300 chained clients, not a defect of either), so its W / p bound is 3e-5;
-# every other case keeps W_RTOL / P_RTOL.
-HORIZON_RTOL = {'horizon_qmc_seq': 3e-5}
+# The solver-horizon cases (make_golden.py HORIZON) run up to 31,300 dependent p-SGD steps and
+# up to 10,000 chained client trainings: there the fp32 arithmetic itself moves a result by more
+# than 1e-5.  Their bounds are DERIVED, per case and quantity, by tests/golden/horizon_drift.py:
+# the CPU restatement run in float32 and in float64 on the same inputs and RNG stream, delta =
+# max over rounds of the relative distance of the two (how far any correct fp32 evaluation sits
+# from the exact one at that horizon), bound = max(1e-5, 2 delta) -- two fp32 evaluations with
+# different summation orders (the reference's torch kernels, the oracle's numpy, the GPU's
+# MFMA) may each be delta away (horizon_drift.json: e.g. horizon_qmc_seq W 1.4e-4, p 3.6e-5;
+# horizon_qmc1000_par W 3.7e-5).  W_RTOL / P_RTOL elsewhere.
+with open(os.path.join(GOLDEN, 'horizon_drift.json')) as _f:
+    HORIZON_DRIFT = json.load(_f)
 
 
-def horizon_rtol(name):
-    return HORIZON_RTOL.get(name, W_RTOL)
+def horizon_rtol(name, what='W'):
+    """The derived bound of a horizon case for ``what`` in 'W', 'p', 'loss' (default bounds for
+    any other case)."""
+    rec = HORIZON_DRIFT.get(name)
+    if rec is None:
+        return {'W': W_RTOL, 'p': P_RTOL, 'loss': LOSS_RTOL}[what]
+    return rec['rtol_' + what]
 
 
 def acc_tol(d):

@@ -443,6 +443,18 @@ HORIZON = {
     # model's), where no fp32 restatement can follow it
     'qmc': dict(data=dict(seed=51, n_test=200, n_raw=12, D=32, C=10, val_frac=0.2), N=300, size_range=(20, 31),
                 hp=dict(lr=0.2, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=20, lr_p=3e-4)),
+    # config 5's EXACT solver instance: N = 1000 -> qmc on K = 16
+    # workgroups of 64 clients (4 per lane), the 16-partner hop config 5 runs; C = 10, n_v ~ 5,000,
+    # R = 10 -> 3,130 dependent momentum steps per round, 31,300 in all.  lr_p: the largest of
+    # 3e-4 / 1e-4 at which the reference's own chained run stays finite (1,000 similar client
+    # models: the p-Hessian is ~N times a single model's)
+    'qmc1000': dict(data=dict(seed=53, n_test=200, n_raw=12, D=32, C=10, val_frac=0.2), N=1000, size_range=(20, 31),
+                    hp=dict(lr=0.2, epoch=2, batch_size=32, prox=False, mu=0.0, reg=True, lam=1e-4, R=10, lr_p=1e-4),
+                    # parallel clients: at 1e-4 p runs to [-0.28, 0.06] and the aggregate of 1,000
+                    # models with such weights cancels -- fp32 and fp64 runs of the same restatement
+                    # part by 23% of max|W| after round 4 (tests/golden/horizon_drift.py): no fp32
+                    # evaluation is reproducible there, so this mode runs at a smaller lr_p
+                    lr_p_par=float(os.environ.get('QMC1000_LR_P_PAR', '2e-5'))),
     # config 1's solver (bin: N <= 16, C = 2) at config 1's shape: 10 label-skewed clients over
     # a9a's 32,561 rows (n_v ~ 6,500), R = 10 -> >= 4,000 steps per round
     'bin': dict(data=dict(seed=52, n_test=300, n_raw=16, D=32, C=2, val_frac=0.2), N=10, total=32561,
@@ -485,9 +497,11 @@ def run_horizon(names=('qmc', 'bin'), modes=('seq', 'par')):
             _trace['W'].clear()
             _trace['p'].clear()
             torch.manual_seed(TORCH_SEED)
+            lr_p = h.get('lr_p_par', hp['lr_p']) if mode == 'par' else hp['lr_p']
             with contextlib.redirect_stdout(io.StringIO()):
-                tr, tl, ta = {'seq': T.FedAMW, 'par': _fedamw_par}[mode](Xs, ys, Xt, yt, vl, *pos, hp['lr_p'])
+                tr, tl, ta = {'seq': T.FedAMW, 'par': _fedamw_par}[mode](Xs, ys, Xt, yt, vl, *pos, lr_p)
             rec = {k: np.asarray(v) for k, v in hp.items()}
+            rec['lr_p'] = np.asarray(lr_p)
             rec.update(algo='fedamw', mode=mode, solver=name, train_loss=tr.detach().numpy(), test_loss=tl.numpy(),
                        test_acc=ta.numpy(), W=np.stack(_trace['W']), p=np.stack(_trace['p']), n_val=nv,
                        steps_per_round=steps, rng_after=torch.empty(4, dtype=torch.int64).random_().numpy())

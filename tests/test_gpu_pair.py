@@ -99,7 +99,9 @@ def test_pair_planner_and_train_form(amd):
 
     P = amd.lib.G_PAIR
     assert plan(100, 10, 32, 2048, 0)[0] == 2                        # config 2: one client per group
-    assert plan(1250, 10, 32, 2048, 0)[0] == 4 | P                   # config 4
+    assert plan(1250, 10, 32, 2048, 0)[0] == 2 | amd.lib.G_PIPE      # config 4: the pipe form (ABI 14)
+    with amd.lib.tuning(split_pipe=-1):
+        assert plan(1250, 10, 32, 2048, 0)[0] == 4 | P               # ... the pair form without it
     assert plan(1000, 7, 32, 4096, 0)[0] == 8 | P                    # config 3
     assert plan(300, 10, 32, 1024, 0)[0] == 2 | P
     with amd.lib.tuning(train_form=2):

@@ -21,7 +21,7 @@ def _pipe(amd, G):
     return G | amd.lib.G_PIPE
 
 
-@pytest.mark.parametrize('G', [2, 4])
+@pytest.mark.parametrize('G', [2, 4, 8, 16])
 @pytest.mark.parametrize('B', [32, 20])
 @pytest.mark.parametrize('C', [10, 16, 2])
 @pytest.mark.parametrize('reg', [False, True])
@@ -30,6 +30,8 @@ def test_pipe_bitwise_equals_split(amd, G, B, C, reg, chained):
     """Pipe form == split form at width G, bitwise: D = 1024 G - 24 (the padded columns stay 0),
     ragged clients incl. tail batches of 1 and 7 rows and an empty client, chained and parallel
     clients, ridge on and off (FedAMW's local training carries the ridge term)."""
+    if G >= 8 and 32 * C + 2 > 512:
+        pytest.skip('the split form exchanges at most 512 values at G >= 8 (C = %d does not fit)' % C)
     rs = np.random.RandomState(G + B + 3 * C + 7 * reg + 11 * chained)
     D, E = 1024 * G - 24, 2
     sizes = [65, 33, 0, 7, 96, 40, 1, 17, 64]
@@ -44,7 +46,7 @@ def test_pipe_bitwise_equals_split(amd, G, B, C, reg, chained):
     assert np.array_equal(lp, ls), np.abs(lp - ls).max()
 
 
-@pytest.mark.parametrize('N,G', [(301, 2), (700, 4)])
+@pytest.mark.parametrize('N,G', [(301, 2), (700, 4), (300, 16)])
 def test_pipe_many_clients(amd, N, G):
     """More clients than groups: every group walks several clients (LPT order, snake over the
     groups), restarting from W_start at each; the next client's rows stream during the previous
@@ -114,6 +116,7 @@ def test_pipe_planner(amd):
     P = amd.lib.G_PIPE
     assert plan(100, 10, 32, 2048, want=2 | P)[0] == 2 | P
     assert plan(100, 10, 32, 4096, want=4 | P)[0] == 4 | P
+    assert plan(1000, 10, 32, 16384, want=16 | P)[0] == 16 | P
     assert plan(10, 2, 32, 2048, chained=1, want=2 | P)[0] == 2 | P
     for args in [dict(B=16), dict(B=32, prox=1), dict(B=32, ld=1024 * 2 + 64), dict(B=32, C=17)]:
         a = dict(N=100, C=10, B=32, ld=2048)
