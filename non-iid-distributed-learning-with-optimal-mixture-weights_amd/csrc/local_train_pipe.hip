@@ -92,8 +92,9 @@ __device__ __forceinline__ void pp_own(T& x) {
 
 __device__ __forceinline__ float invb_of(int bc) { return 1.0f / (float)bc; }
 
-template <int G, bool NRM>
+template <int G, bool NRM, bool PROX>
 __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParams P, SplitWS X) {
+  static_assert(NRM || !PROX, "the prox term exchanges the norms");
   constexpr int NW = PP_WAVES, TPW = PP_TPW, RS = PP_RS, NC = 16;
   constexpr int GP = G > 1 ? G - 1 : 1;          // partners
   // wave partial logits, transposed: zpt[w][rt][class * ZS + 4 lg + kk] = the partial of row
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   __shared__ __attribute__((aligned(16))) float gsm[2][2][64][4];
   __shared__ __attribute__((aligned(16))) unsigned gfl[2][2][4];
   __shared__ float cesm[2][8];             // per 4-row group CE wave sums (the reported loss)
-  __shared__ float wn2sm[2];               // ||W||^2 at the step's start (ridge), by wave 0
+  __shared__ float wn2sm[2][2];            // ||W - W_a||^2, ||W||^2 at the step's start, by wave 0
   __shared__ float wred[NW][2];            // ||W - W_a||^2 (always 0 here), ||W||^2 of the wave's slice
   extern __shared__ __attribute__((aligned(16))) float xs_dyn[];   // [32][RS] batch slice image
 
@@ -285,7 +286,9 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   // rows of rt1 2 + 1 + NRM, the indices 1 + NRM + 1.  A stale poll is re-polled with nothing
   // else in flight.  Other extra operations (client-end stores, spills) only make a wait
   // stricter.
-  constexpr int W_F0 = 8 + 2, W_F1 = 2 + 1 + (NRM ? 1 : 0), W_IDX = 1 + (NRM ? 1 : 0) + 1;
+  // PROX: 8 anchor loads (the client's start W_a, tools.py:180; L2-resident) go out right after
+  // the labels -- the update waits for them with the 16 row loads of K0 and K1 behind.
+  constexpr int W_F0 = 8 + 2, W_F1 = 2 + 1 + (NRM ? 1 : 0), W_IDX = 1 + (NRM ? 1 : 0) + 1, W_ANC = 16;
   const int hrt = w >> 2, kcol = w & 3;          // this wave's softmax column: row tile, kk
 
   SpCur cc;
@@ -297,6 +300,8 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   const int rblk = 4 * (l16 & 3) + (l16 >> 2);
   unsigned long long pl[GP];
   unsigned long long pnrm[GP];
+  floatx4 av[TPW][4];                            // PROX: the anchor slice of this step
+  const float* anc = P.W_start;                  // PROX: the anchor of the current client
 #ifdef FS_STAMPS
   unsigned long long stamp_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
 #endif
@@ -310,6 +315,9 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
       } else if (lane == 0) {
         wred[w][0] = 0.f;
       }
+      // the prox anchor is the client's start (tools.py:180): W_start, or in a chain the previous
+      // client's result, which this workgroup stored at that client's end
+      if (PROX) anc = (P.chained && cc.j > 0) ? P.W_out + (int64_t)(cc.j - 1) * C * ld : start;
       lsum = 0.0;
     }
     const int e = st / nbat, s = st - e * nbat;
@@ -477,7 +485,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
             if (k + (k >= g ? 1 : 0) == h) pv = __uint_as_float((unsigned)pnrm[k]);
           ns += (h == g) ? mine : pv;
         }
-        if (lane == 1) wn2sm[par] = ns;
+        if (lane < 2) wn2sm[par][lane] = ns;
       }
       // the softmax of (row 16 hrt + 4 kcol + lg, class l16) -- the split form's arithmetic: its
       // xor butterflies 8, 4, 2, 1 over the class lanes with the same bits (the max is exact in
@@ -508,8 +516,15 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
       if (lane == 0) gfl[par][hrt][kcol] = tag32;
     }
     // the next step's labels (the polls have all landed and this step's labels are read: nothing
-    // of ours waits behind them)
+    // of ours waits behind them); PROX: this step's anchor slice
     issue_labels();
+    if (PROX) {
+      int64_t b = (int64_t)min(l16, C - 1) * ld + 64 * t0 + 4 * lg + 64 * w;
+      asm volatile("" : "+v"(b));
+      const float* a = anc + b;
+      pp_ld4<0>(av[0][0], a); pp_ld4<64>(av[0][1], a); pp_ld4<128>(av[0][2], a); pp_ld4<192>(av[0][3], a);
+      pp_ld4<2048>(av[1][0], a); pp_ld4<2112>(av[1][1], a); pp_ld4<2176>(av[1][2], a); pp_ld4<2240>(av[1][3], a);
+    }
     PP_STAMP(11)
     // ---- the g values of a row tile, once its four columns are flagged ----
     float gB[8];
@@ -569,8 +584,11 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     bwd(0, 0);                                      // K0 (beside the other half's round trip)
     PP_STAMP(13)
     take_g(1);
-    float wn2 = 0.f;
-    if (NRM) wn2 = wn2sm[par];
+    float pn2 = 0.f, wn2 = 0.f;
+    if (NRM) {
+      pn2 = wn2sm[par][0];
+      wn2 = wn2sm[par][1];
+    }
     if (need_ce && w == 0) {
       // the loss as the split form sums it: the eight 4-row-group CE sums in row order
       float ce = 0.f;
@@ -578,27 +596,48 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
       for (int k = 0; k < 8; ++k) ce += cesm[par][k];
       if (lane == 0) {
         float loss = ce / (float)bc;
+        if (P.prox) loss = loss + P.mu * sqrtf(pn2);
         if (P.reg) loss = loss + P.lam * sqrtf(wn2);
         lsum += (double)loss * (double)bc;
       }
     }
     bwd(4, 1);                                      // K1
     // ---- update of the register-resident slice ----
+    float npn = 0.f, nwn = 0.f;
     {
+      const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;
       const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
       const float lr = P.lr;
+      if (PROX) {
+        pp_wait<W_ANC>();                           // the anchor slice landed
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pp_own(av[i][q]);
+      }
       if (l16 < C) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4) wr[i][q][e4] = sgd_w(wr[i][q][e4], ga[i][e4][q], lr, false, 0.f, 0.f, P.reg, sr);
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const float ac = PROX ? av[i][q][e4] : 0.f;
+              const float o = sgd_w(wr[i][q][e4], ga[i][e4][q], lr, PROX, ac, sp, P.reg, sr);
+              wr[i][q][e4] = o;
+              if (PROX) {                            // the split form's inline norms (its order)
+                npn = sq_acc(npn, o - ac);
+                nwn = sq_acc(nwn, o);
+              }
+            }
       }
     }
-    if (NRM) {
+    if (PROX) {
+      npn = wave_sum_dpp(npn, lane);
+      nwn = wave_sum_dpp(nwn, lane);
+      if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
+    } else if (NRM) {
       // ridge: ||W||^2 of the updated slice in the update's order (the split form's bits)
-      float nwn = 0.f;
 #pragma unroll
       for (int i = 0; i < TPW; ++i)
 #pragma unroll
@@ -630,8 +669,9 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
 }
 
 bool pipe_fits(int C, int B, int NT, int G, int prox) {
+  (void)prox;
   if (!(G == 2 || G == 4 || G == 8 || G == 16)) return false;
-  return !prox && C >= 1 && C <= 16 && B > 16 && B <= 32 && NT == PP_NTS * G;
+  return C >= 1 && C <= 16 && B > 16 && B <= 32 && NT == PP_NTS * G;
 }
 
 static int64_t pipe_xbuf_bytes(int ngroups, int G) { return (int64_t)ngroups * 2 * G * PP_SZ * 8; }
@@ -642,17 +682,18 @@ int64_t pipe_ws_bytes(int N, int G, int chained, int cus) {
   return pipe_xbuf_bytes(pipe_groups(N, G, chained, cus), G) + PP_ERR_BYTES;
 }
 
-template <int G, bool NRM>
+template <int G, bool NRM, bool PROX>
 static void launch_pipe_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_pipe_kernel<G, NRM>),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_pipe_kernel<G, NRM, PROX>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_pipe_kernel<G, NRM>), dim3(grid), dim3(PP_THREADS), lds, st, P, X);
+  hipLaunchKernelGGL((local_train_pipe_kernel<G, NRM, PROX>), dim3(grid), dim3(PP_THREADS), lds, st, P, X);
 }
 
 template <int G>
 static void launch_pipe_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  if (P.reg) launch_pipe_s<G, true>(P, X, grid, lds, st);
-  else launch_pipe_s<G, false>(P, X, grid, lds, st);
+  if (P.prox) launch_pipe_s<G, true, true>(P, X, grid, lds, st);
+  else if (P.reg) launch_pipe_s<G, true, false>(P, X, grid, lds, st);
+  else launch_pipe_s<G, false, false>(P, X, grid, lds, st);
 }
 
 unsigned split_spin_bound();   // local_train_split.hip: fs_tuning.spin_limit / the test knob
@@ -660,8 +701,8 @@ unsigned split_spin_bound();   // local_train_split.hip: fs_tuning.spin_limit / 
 int launch_local_train_pipe(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st) {
   const int NT = (int)(P.ld >> 6);
   if (!pipe_fits(P.C, P.B, NT, G, P.prox))
-    return fail(FS_EUNSUPPORTED, "fs_local_train: the pipe form needs ld = 1024 G (G = 2, 4, 8 or 16), 16 < B <= 32, "
-                                 "C <= 16 and no prox term");
+    return fail(FS_EUNSUPPORTED, "fs_local_train: the pipe form needs ld = 1024 G (G = 2, 4, 8 or 16), 16 < B <= 32 "
+                                 "and C <= 16");
   const int cus = device_cus();
   if (cus <= 0) return fail(FS_EHIP, "fs_local_train: no device");
   if (G > cus) return fail(FS_EUNSUPPORTED, "fs_local_train: G exceeds the CU count");

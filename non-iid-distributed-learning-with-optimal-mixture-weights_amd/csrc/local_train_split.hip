@@ -908,7 +908,7 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   if (!(want > 1 && want < FS_G_PAIR) && NT % 16 == 0 && tuning().split_pipe >= 0) {
     const int g = NT / 16;
     const bool by_shape = tuning().split_pipe == 0 && want == 0 && tuning().train_form == 0 && !chained &&
-                          g <= 4 && N > pipe_groups(N, g, 0, cus);
+                          !prox && g <= 4 && N > pipe_groups(N, g, 0, cus);
     if ((tuning().split_pipe > 0 || by_shape) && pipe_fits(C, B, NT, g, prox) && g <= cus) {
       *G_out = g | FS_G_PIPE;
       *ws_bytes_out = pipe_ws_bytes(N, g, chained, cus);

@@ -5,7 +5,7 @@ hand-off pipelined by 16-row tile and the softmax computed per wave in registers
 runs the split form's arithmetic at the same width in the same order, so the two forms must
 agree BITWISE (weights and losses) on every covered shape -- and the split form is itself pinned
 to the oracle and the reference fixtures (test_gpu_parity.py).  Reference: train_loop,
-/root/reference/functions/tools.py:177-215 (FedAvg / FedAMW local training: no prox term).
+/root/reference/functions/tools.py:177-215 (FedAvg / FedAMW local training; FedProx's prox term).
 """
 import numpy as np
 import pytest
@@ -24,23 +24,25 @@ def _pipe(amd, G):
 @pytest.mark.parametrize('G', [2, 4, 8, 16])
 @pytest.mark.parametrize('B', [32, 20])
 @pytest.mark.parametrize('C', [10, 16, 2])
-@pytest.mark.parametrize('reg', [False, True])
+@pytest.mark.parametrize('terms', ['', 'reg', 'prox', 'prox+reg'])
 @pytest.mark.parametrize('chained', [False, True])
-def test_pipe_bitwise_equals_split(amd, G, B, C, reg, chained):
+def test_pipe_bitwise_equals_split(amd, G, B, C, terms, chained):
     """Pipe form == split form at width G, bitwise: D = 1024 G - 24 (the padded columns stay 0),
     ragged clients incl. tail batches of 1 and 7 rows and an empty client, chained and parallel
-    clients, ridge on and off (FedAMW's local training carries the ridge term)."""
+    clients, ridge on and off (FedAMW's local training carries the ridge term), FedProx's prox
+    term on and off (its anchor: W_start, or in a chain the previous client's result)."""
     if G >= 8 and 32 * C + 2 > 512:
         pytest.skip('the split form exchanges at most 512 values at G >= 8 (C = %d does not fit)' % C)
-    rs = np.random.RandomState(G + B + 3 * C + 7 * reg + 11 * chained)
+    reg, prox = 'reg' in terms, 'prox' in terms
+    rs = np.random.RandomState(G + B + 3 * C + 7 * reg + 11 * chained + 13 * prox)
     D, E = 1024 * G - 24, 2
     sizes = [65, 33, 0, 7, 96, 40, 1, 17, 64]
     Xs, ys = _rand_clients(rs, sizes, D, C)
     W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
-    lr, lam = 0.4, 0.002
-    Wp, lp = _train_via_abi(amd, Xs, ys, W0, lr, E, B, False, 0.0, reg, lam, chained, seed=3, split=_pipe(amd, G))
+    lr, lam, mu = 0.4, 0.002, 0.05
+    Wp, lp = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=3, split=_pipe(amd, G))
     assert _train_via_abi.last_G == _pipe(amd, G)
-    Ws, ls = _train_via_abi(amd, Xs, ys, W0, lr, E, B, False, 0.0, reg, lam, chained, seed=3, split=G)
+    Ws, ls = _train_via_abi(amd, Xs, ys, W0, lr, E, B, prox, mu, reg, lam, chained, seed=3, split=G)
     assert _train_via_abi.last_G == G
     assert np.array_equal(Wp, Ws), np.abs(Wp - Ws).max()
     assert np.array_equal(lp, ls), np.abs(lp - ls).max()
@@ -102,7 +104,7 @@ def test_pipe_timeout_raises(amd):
 
 def test_pipe_planner(amd):
     """fs_local_train_plan: an explicit pipe request is honoured where the form covers the shape
-    (ld = 1024 G, 16 < B <= 32, C <= 16, no prox) and falls back to the planner's own choice
+    (ld = 1024 G, 16 < B <= 32, C <= 16) and falls back to the planner's own choice
     elsewhere; fs_tuning.split_pipe = 1 picks it wherever it fits, -1 never."""
     import ctypes
     L = amd.lib.lib()
@@ -118,7 +120,8 @@ def test_pipe_planner(amd):
     assert plan(100, 10, 32, 4096, want=4 | P)[0] == 4 | P
     assert plan(1000, 10, 32, 16384, want=16 | P)[0] == 16 | P
     assert plan(10, 2, 32, 2048, chained=1, want=2 | P)[0] == 2 | P
-    for args in [dict(B=16), dict(B=32, prox=1), dict(B=32, ld=1024 * 2 + 64), dict(B=32, C=17)]:
+    assert plan(100, 7, 32, 4096, prox=1, want=4 | P)[0] == 4 | P
+    for args in [dict(B=16), dict(B=32, ld=1024 * 2 + 64), dict(B=32, C=17)]:
         a = dict(N=100, C=10, B=32, ld=2048)
         a.update(args)
         assert not plan(want=2 | P, **a)[0] & P, args
