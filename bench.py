@@ -107,6 +107,8 @@ def parse(argv=None):
     ap.add_argument('--teardown-timeout', type=float, default=300.0,
                     help='--gpus N launcher: once a worker has exited 0, the seconds the others get to finish '
                          '(a rank hung in a collective or in teardown); exit code 124 when it trips (0 = none)')
+    ap.add_argument('--no-eval-fuse', action='store_true',
+                    help='fs_tuning.no_eval_fuse = 1: the deferred evaluation in launches of its own (PMC traffic split)')
     ap.add_argument('--split-early', choices=['auto', 'off'], default='auto',
                     help="fs_tuning.split_early: the split form's early row issue (A/B runs)")
     a = ap.parse_args(argv)
@@ -568,6 +570,9 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
     achieved = alg_bytes / (lt_ms * 1e-3) / 1e9 if lt_ms else float('nan')
     tag = 'c%d%s' % (cfg, '' if algo == PRESETS[cfg]['algo'] else '_' + algo)
     rec, tnote = (None, 'custom workload') if custom else load_record(tag, 'local_train')
+    # the same workload captured with fs_tuning.no_eval_fuse = 1: the training launch's own bytes,
+    # without the deferred test-set evaluation the default plan carries inside it
+    nrec, _ = (None, None) if custom else load_record(tag + '_nofuse', 'local_train')
     total = N_loc * ws
     out = {
         'value': total * steps / el,
@@ -584,6 +589,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
         'roofline': {'kernel': 'fs_local_train', 'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                      'traffic': (rec or {}).get('bytes_per_launch'), 'traffic_note': tnote,
+                     'traffic_no_eval_fuse': (nrec or {}).get('bytes_per_launch'),
                      'mfma_busy': (rec or {}).get('mfma_busy'),
                      'launch_ms': lt_ms, 'alg_bytes_per_launch': alg_bytes, 'group_width': fed.trainer.width,
                      'form': 'pair' if fed.trainer.pair else ('teams' if fed.trainer.teams else
@@ -642,7 +648,7 @@ def worker(args):
     flib.set_tuning(train_form={'auto': 0, 'split': 1, 'pair': 2, 'teams': 1, 'pipe': 1}[args.train_form],
                     split_teams={'auto': 0, 'split': -1, 'pair': -1, 'teams': 1, 'pipe': -1}[args.train_form],
                     split_pipe={'auto': 0, 'split': -1, 'pair': -1, 'teams': -1, 'pipe': 1}[args.train_form],
-                    split_early={'auto': 0, 'off': -1}[args.split_early])
+                    split_early={'auto': 0, 'off': -1}[args.split_early], no_eval_fuse=int(args.no_eval_fuse))
     wl = {k: getattr(args, k) for k in ('algo', 'clients', 'rows', 'D', 'C', 'test', 'shape')}
     wl['config'] = args.config
     headline = (args.config == 2 and not args.custom)

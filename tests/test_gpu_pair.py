@@ -91,9 +91,9 @@ def test_pair_planner_and_train_form(amd):
     import ctypes
     L = amd.lib.lib()
 
-    def plan(N, C, B, ld, chained, want=0):
+    def plan(N, C, B, ld, chained, want=0, prox=0):
         g, w = ctypes.c_int(want), ctypes.c_int64(0)
-        amd.lib.check(L.fs_local_train_plan(N, C, B, 2, ld, 1024, chained, 0, ctypes.byref(g), ctypes.byref(w)),
+        amd.lib.check(L.fs_local_train_plan(N, C, B, 2, ld, 1024, chained, prox, ctypes.byref(g), ctypes.byref(w)),
                       'plan')
         return g.value, w.value
 
@@ -102,7 +102,8 @@ def test_pair_planner_and_train_form(amd):
     assert plan(1250, 10, 32, 2048, 0)[0] == 2 | amd.lib.G_PIPE      # config 4: the pipe form (ABI 14)
     with amd.lib.tuning(split_pipe=-1):
         assert plan(1250, 10, 32, 2048, 0)[0] == 4 | P               # ... the pair form without it
-    assert plan(1000, 7, 32, 4096, 0)[0] == 8 | P                    # config 3
+    assert plan(1000, 7, 32, 4096, 0, prox=1)[0] == 8 | P            # config 3 (FedProx: the pair form)
+    assert plan(1000, 7, 32, 4096, 0)[0] == 4 | amd.lib.G_PIPE       # ... its shape without the prox term
     assert plan(300, 10, 32, 1024, 0)[0] == 2 | P
     with amd.lib.tuning(train_form=2):
         assert plan(100, 10, 32, 2048, 0)[0] == 4 | P
