@@ -16,19 +16,22 @@
 // rt0's round trip runs under F1, rt1's under K0 (the polls are issued after a whole MFMA
 // phase and are normally fresh at once), and the next step's rows stream from the image write
 // on (rt0) and from K0's end on (rt1) instead of only inside the backward.
-//   * every wave computes the softmax of all 16 rows of a tile itself, in registers, in the
-//     backward's operand layout (lane (class, lg) holds rows 4 kk + lg of the tile, kk = 0..3:
-//     exactly the g values its backward MFMAs take), from the own slice's partial logits (an
-//     LDS transpose of the 8 wave partials, summed in wave order) plus the partners' granules
-//     it polls itself (G - 1 partners x 4 per lane) -- no S2 / S3 barrier, no LDS gbuf;
+//   * each wave computes the softmax of ONE 16-lane-row column of a tile (row tile w / 4, rows
+//     4 (w % 4) + lg) in registers, from the own slice's partial logits (an LDS transpose of the
+//     8 wave partials, summed in wave order) plus the partners' granules it polls itself (G - 1
+//     per lane), and hands its g values to the other waves through LDS with a tag flag per
+//     column (no barrier): waves 0-3 finish tile 0's softmax while waves 4-7 still wait for
+//     tile 1's partners;
 //   * two barriers per step (one per row tile: the wave partials); the LDS image is
 //     wave-private (each wave reads back only its own tiles), so it needs none;
 //   * the same {tag, value} granule hand-off as the split form (cdna_hip_programming.md
 //     Guideline 16, R2: relaxed agent-scope store / load, the data is its own flag), the
 //     partner sum in slice order with the own partial at position g, every spin bounded.
 // Covered shapes: full slices (ld = 1024 G: 16 tiles per workgroup, 2 per wave), 16 < B <= 32,
-// C <= 16, no FedProx anchor (FedAvg, FedAMW's ridge-regularised local training: configs 2, 4
-// and 5).  The bitwise match with the split form is tested (tests/test_gpu_pipe.py).
+// C <= 16; the ridge and FedProx terms (the prox anchor's slice streamed per step, round 5).
+// The bitwise match with the split form is tested (tests/test_gpu_pipe.py).  The planner picks
+// it by shape only where it measured fastest (parallel clients at G <= 4 with more clients than
+// groups and no prox term: config 4).
 #include <type_traits>
 
 #include "common.h"
