@@ -222,8 +222,8 @@ int fs_randperm_device(const int64_t* d_seeds, const int64_t* d_n, const int64_t
  *              teams of 4 that train two clients at once with team-local barriers, so one
  *              team's hand-off and softmax run beside the other team's MFMAs (the split
  *              arithmetic with 4 waves per slice: within the fp32 tolerance of the split form).
- *              G | FS_G_PIPE (ABI 14, ld == 1024 G with G = 2, 4, 8 or 16, 16 < B <= 32, C <= 16, no
- *              prox term; parallel or chained clients): the "pipe" form -- the split form with
+ *              G | FS_G_PIPE (ABI 14, ld == 1024 G with G = 2, 4, 8 or 16, 16 < B <= 32, C <= 16;
+ *              parallel or chained clients, ridge and prox terms): the "pipe" form -- the split form with
  *              each step's hand-off pipelined by 16-row tile (one tile's partner round trip under
  *              the other tile's forward or backward MFMAs, the softmax per wave in registers, two
  *              barriers per step); the same arithmetic in the same order as the split form at
