@@ -256,7 +256,8 @@ KERNEL_SOURCES = {
 
 
 def source_revision(kernel=None):
-    """sha256 (16 hex digits) of device sources of libfedsim.so: all of them (csrc/*.hip,
+    """sha256 (16 hex digits) of the code (comments and whitespace runs dropped) of the device
+    sources of libfedsim.so: all of them (csrc/*.hip,
     csrc/*.h; host-only .cpp files and the C-ABI header carry no device code), or only those
     ``kernel`` ('local_train', 'mix_solve') is compiled from.  Profiles under profiles/
     record it; bench.py uses a PMC traffic figure only when it was measured on the kernel's
@@ -272,8 +273,31 @@ def source_revision(kernel=None):
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, 'rb') as fh:
-            h.update(fh.read())
+            h.update(_code_only(fh.read().decode()).encode())
     return h.hexdigest()[:16]
+
+
+_TOKENS = None
+
+
+def _code_only(src):
+    """The source without comments and with whitespace runs collapsed (string and character
+    literals kept verbatim): a comment edit does not change a kernel's revision."""
+    global _TOKENS
+    import re
+    if _TOKENS is None:
+        _TOKENS = re.compile(r'"(?:\\.|[^"\\])*"|\'(?:\\.|[^\'\\])*\'|//[^\n]*|/\*.*?\*/|\s+|[^"\'/\s]+|/',
+                             re.S)
+    out = []
+    for m in _TOKENS.finditer(src):
+        t = m.group(0)
+        if t.startswith('//') or t.startswith('/*'):
+            out.append(' ')
+        elif t.isspace():
+            out.append(' ')
+        else:
+            out.append(t)
+    return re.sub(r' +', ' ', ''.join(out)).strip()
 
 
 class Timer:

@@ -157,3 +157,15 @@ def test_tuning_context_on_a_thread_with_an_override():
         assert _lib.get_process_tuning()['mix_prefetch'] == 0
     finally:
         _lib.set_tuning(**prev)
+
+
+def test_source_revision_ignores_comments():
+    """bench.py keys a PMC capture to the code it measured (_lib.source_revision): a comment or
+    whitespace edit keeps the key, a code edit changes it; literals are kept verbatim."""
+    c = _lib._code_only
+    base = 'int a = 1; // one\n/* two\n three */ float b = a / 2;\n'
+    assert c(base) == c('int a = 1;\n\n  float b = a / 2; // changed comment\n')
+    assert c(base) != c(base.replace('a / 2', 'a / 3'))
+    assert c('const char* s = "x // y";') == 'const char* s = "x // y";'
+    assert c("asm(\"s_waitcnt vmcnt(0) ; pr-own\"); char q = '/';") == "asm(\"s_waitcnt vmcnt(0) ; pr-own\"); char q = '/';"
+    assert re.fullmatch(r'[0-9a-f]{16}', _lib.source_revision('local_train'))
