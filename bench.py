@@ -72,7 +72,7 @@ PRESETS = {
 }
 STRONG = {5}
 # the extra legs of the default run: (config, timed rounds, warmup rounds)
-LEGS = ((4, 10, 2), (3, 5, 1), (5, 2, 1))
+LEGS = ((4, 10, 10), (3, 5, 2), (5, 2, 1))     # (config, timed rounds, warm-up rounds)
 
 
 def parse(argv=None):
@@ -261,6 +261,38 @@ def load_record(tag, kernel):
     return rec, 'PMC %s' % rec.get('source', '')
 
 
+def settle_clocks(dev, ms):
+    """Hold the GPU busy for ``ms`` milliseconds of plain fp32 GEMMs and 1 GiB device copies (no
+    part of the workload: nothing of it is computed, cached or skipped) before a measurement's
+    warm-up rounds.  From idle the device takes tens of ms of sustained load to reach its
+    steady clocks: config 2 at the driver's --warmup 5 ran 0.311-0.317 ms per round, after 100 ms
+    of this settle 0.299-0.302, after 50 / 200 warm-up rounds of the workload itself 0.292 / 0.290
+    (profiles/r05/warmup_ab.txt) -- a 20-round timed region would otherwise measure part of the
+    clock ramp.  Reported on the line as ``device_settle_ms``; FS_BENCH_SETTLE_MS overrides the
+    length (0 = off), FS_BENCH_SETTLE_KIND = gemm | copy | mixed the load."""
+    ms = float(os.environ.get('FS_BENCH_SETTLE_MS', ms))
+    if ms <= 0 or dev.type != 'cuda':
+        return 0.0
+    import torch
+    kind = os.environ.get('FS_BENCH_SETTLE_KIND', 'mixed')           # GEMMs and 1 GiB copies
+    a = torch.randn(4096, 4096, device=dev)
+    b = torch.randn(4096, 4096, device=dev)
+    x = torch.empty(256 << 20, dtype=torch.float32, device=dev)      # 1 GiB streamed
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        if kind in ('gemm', 'mixed'):
+            for _ in range(2):
+                a = torch.mm(a, b) * 1e-3
+        if kind in ('copy', 'mixed'):
+            y.copy_(x)
+            x.copy_(y)
+        torch.cuda.synchronize()
+    del x, y
+    return (time.perf_counter() - t0) * 1e3
+
+
 def phase_ms(events, name):
     v = [a.elapsed_time(b) for n, a, b in (events or []) if n == name]
     return float(np.mean(v)) if v else None
@@ -432,6 +464,7 @@ def config1_leg(dev, rounds=10, warmup=2, cpu_budget=3.0):
     fed = tools.Federation('fedamw', d['X_train'], d['y_train'], d['X_test'], d['y_test'], d['validloader'],
                            'classification', C, D, lr, E, B, False, 0.0, True, lam, R, lr_p, 'sequential',
                            verbose=False)
+    settled = settle_clocks(dev, 100.0)
     for _ in range(warmup):
         fed.round()
     torch.cuda.synchronize()
@@ -455,6 +488,7 @@ def config1_leg(dev, rounds=10, warmup=2, cpu_budget=3.0):
            'p_solve_us_per_step': 1e3 * solve_ms / steps if solve_ms else None,
            'p_solver': fedamw_amd._lib.SOLVER_NAMES.get(fedamw_amd._lib.lib().fs_mix_solve_last_mode(), '?'),
            'local_train_group_width': fed.trainer.width, 'final_test_acc': float(ta[fed.t - 1]),
+           'device_settle_ms': settled,
            'context': 'BASELINE.md: the reference CPU path runs this round in 20.0 s = 0.50 client-rounds/s on '
                       '8 Xeon cores (survey container; not a published number)'}
     if cpu_budget > 0:
@@ -545,10 +579,13 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                            E, B, algo == 'fedprox', mu, fedamw, 1e-5, R, 1e-3,
                            'parallel', verbose=False, shuffle_device=not host_shuffle)
     assert len(fed.mine) == N_loc
+    settled = settle_clocks(dev, 100.0)
     for _ in range(warmup):
         fed.round()
     torch.cuda.synchronize()
-    fed.events = []
+    # (FS_BENCH_NO_EVENTS=1: no per-launch timing events -- an A/B of their own cost; the line's
+    # roofline then has no launch time)
+    fed.events = None if os.environ.get('FS_BENCH_NO_EVENTS') == '1' else []
     if ws > 1:
         tdist.barrier()
     torch.cuda.synchronize()
@@ -596,6 +633,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                                                               ('pipe' if fed.trainer.pipe else
                                                                ('split' if fed.trainer.G > 1 else 'single')))},
         'final_test_acc': float(ta[fed.t - 1]),
+        'device_settle_ms': settled,
     }
     if fedamw:
         nv = fed.mixture.nv
@@ -674,6 +712,7 @@ def worker(args):
         'dist': dinfo,
         'roofline': main['roofline'],
         'final_test_acc': main['final_test_acc'],
+        'device_settle_ms': main['device_settle_ms'],
     }
     for k in ('fedamw', 'cpu_baseline'):
         if k in main:
@@ -686,7 +725,7 @@ def worker(args):
             obj = {'workload': r['workload'], 'value': r['value'], 'unit': 'client-rounds/s',
                    'ms_per_round': r['ms_per_step'], 'rounds_timed': k, 'warmup': w, 'scaling': r['scaling'],
                    'roofline': r['roofline'], 'final_test_acc': r['final_test_acc'],
-                   'leg_wall_s': time.perf_counter() - t0}
+                   'device_settle_ms': r['device_settle_ms'], 'leg_wall_s': time.perf_counter() - t0}
             for key in ('fedamw', 'cpu_baseline'):
                 if key in r:
                     obj[key] = r[key]

@@ -372,7 +372,12 @@ int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, i
  *                       next call's TRAIN launch, on the CUs its client groups
  *                       leave idle (parallel split launches, C <= 16; the same
  *                       per-row arithmetic as fs_eval).  d_eval_hist[2t..] is then
- *                       written by that call.  The pending evaluation reads d_W_g
+ *                       written by that call if it aggregates, else (round 5) by the
+ *                       call after it: the fused evaluation's finaliser rides on the
+ *                       next AGGREGATE launch, and any call that trains or does not
+ *                       aggregate runs a pending one first -- make one more
+ *                       fs_plan_round call (phases 0 will do) before reading
+ *                       d_eval_hist after a TRAIN-only call.  The pending evaluation reads d_W_g
  *                       as it is when that next call's launches run: the caller
  *                       must NOT write d_W_g (its own aggregate, an all-reduce into
  *                       it, a copy) between the deferring call and the next

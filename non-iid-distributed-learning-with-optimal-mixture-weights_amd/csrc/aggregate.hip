@@ -11,6 +11,7 @@
 // range is cut into `chunks` consecutive pieces folded in parallel (stage 1) and the
 // partials are folded by a fixed tree (stage 2: strided in-order sums, then those in order).
 #include "common.h"
+#include "finalize.h"
 
 namespace fs {
 
@@ -82,23 +83,114 @@ __global__ __launch_bounds__(256) void fold_partials_kernel(const float* __restr
   }
 }
 
-}  // namespace fs
+// One-launch form (round 5, chunks <= 0 with 16 <= N <= AG_ONE_MAX_N): SUB consecutive client
+// ranges per float4 position folded by SUB threads of one workgroup (stage 1, as
+// aggregate_kernel's chunks), their partials folded in order in LDS (stage 2) -- one launch
+// instead of two, no workspace.  The round plan also hands it the deferred evaluation's
+// finaliser (one extra workgroup, eval.hip's eval_finalize arithmetic): config 2's round went
+// from four launches after the training (finalise, aggregate, fold, next training) to two.
+constexpr int AG_ONE_MAX_N = 512;   // above: 64 sub-ranges of 4 positions read 64-byte pieces of
+                                    // each client row (N = 1000-1250: 34-38 vs 18-19 us, round 5)
 
-using namespace fs;
+template <int SUB>
+__global__ __launch_bounds__(256) void aggregate_one_kernel(const float* __restrict__ W, int64_t stride,
+                                                           const float* __restrict__ p, int N, int64_t len4, int per,
+                                                           float* __restrict__ out, EvalFinalize fin) {
+  constexpr int POS = 256 / SUB;
+  __shared__ float4 sums[SUB][POS];
+  if (fin.part && blockIdx.x == gridDim.x - 1) {
+    eval_finalize_block(fin.part, fin.nb, fin.n, fin.out, reinterpret_cast<double(*)[256]>(&sums[0][0]));
+    return;
+  }
+  static_assert(sizeof(sums) >= 2 * 256 * sizeof(double), "the finaliser reuses the partials' LDS");
+  const int sub = threadIdx.x / POS, pl = threadIdx.x % POS;
+  const int64_t i = (int64_t)blockIdx.x * POS + pl;
+  const int j0 = sub * per, j1 = min(N, j0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < len4 && j0 < j1) {
+    const float* base = W + 4 * i;
+    const float4 w0 = ld4(base + (int64_t)j0 * stride);
+    const float p0 = p[j0];
+    acc = make_float4(p0 * w0.x, p0 * w0.y, p0 * w0.z, p0 * w0.w);
+    int j = j0 + 1;
+    for (; j + 7 < j1; j += 8) {                 // 8 loads in flight per round trip
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld4(base + (int64_t)(j + u) * stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = fold_step(acc, p[j + u], v[u]);
+    }
+    for (; j + 3 < j1; j += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld4(base + (int64_t)(j + u) * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = fold_step(acc, p[j + u], v[u]);
+    }
+    for (; j < j1; ++j) acc = fold_step(acc, p[j], ld4(base + (int64_t)j * stride));
+  }
+  sums[sub][pl] = acc;
+  __syncthreads();
+  if (sub == 0 && i < len4) {
+    float4 t = sums[0][pl];
+    for (int s2 = 1; s2 < SUB && s2 * per < N; ++s2) {
+      const float4 v = sums[s2][pl];
+      t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+    }
+    st4(out + 4 * i, t);
+  }
+}
 
-extern "C" int fs_aggregate(const float* d_W_all, int64_t stride, const float* d_p, int N, int64_t len,
-                            float* d_W_bar, float* d_ws, int64_t ws_floats, int chunks, void* stream) {
+// sub-ranges per position: 1 below 16 clients (then the fold is the reference's, bitwise),
+// else the largest power of two <= min(32, N / 6) (~6+ clients per thread: one or two round
+// trips of 8 loads)
+static int one_launch_sub(int N) {
+  if (N < 16) return 1;
+  int s = 1;
+  while (s * 2 <= 32 && s * 2 <= N / 6) s *= 2;
+  return s;
+}
+
+template <int SUB>
+static void launch_one(const float* W, int64_t stride, const float* p, int N, int64_t len4, float* out,
+                       const EvalFinalize& fin, hipStream_t st) {
+  constexpr int POS = 256 / SUB;
+  const int per = (N + SUB - 1) / SUB;
+  const int64_t blocks = (len4 + POS - 1) / POS + (fin.part ? 1 : 0);
+  hipLaunchKernelGGL((aggregate_one_kernel<SUB>), dim3((unsigned)blocks), dim3(256), 0, st, W, stride, p, N, len4, per,
+                     out, fin);
+}
+
+int aggregate_launch(const float* d_W_all, int64_t stride, const float* d_p, int N, int64_t len, float* d_W_bar,
+                     float* d_ws, int64_t ws_floats, int chunks, const EvalFinalize* fin, hipStream_t st) {
   FS_REQUIRE(N >= 1, "N must be >= 1");
   FS_REQUIRE(len >= 4 && len % 4 == 0 && stride % 4 == 0 && stride >= len, "len/stride must be multiples of 4");
   FS_REQUIRE(d_W_all && d_p && d_W_bar, "null pointer");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t len4 = len / 4;
+  const EvalFinalize none{nullptr, 0, 0, nullptr};
+  if (chunks <= 0 && N <= AG_ONE_MAX_N) {
+    const EvalFinalize& f = fin ? *fin : none;
+    switch (one_launch_sub(N)) {
+      case 1: launch_one<1>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+      case 2: launch_one<2>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+      case 4: launch_one<4>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+      case 8: launch_one<8>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+      case 16: launch_one<16>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+      default: launch_one<32>(d_W_all, stride, d_p, N, len4, d_W_bar, f, st); break;
+    }
+    FS_LAUNCH_CHECK();
+    return FS_OK;
+  }
+  if (fin) {
+    const int rc = eval_finalize_launch(fin->part, fin->nb, fin->n, fin->out, st);
+    if (rc != FS_OK) return rc;
+  }
   const int64_t bx = (len4 + 255) / 256;
   if (chunks <= 0) {
-    // aim for >= ~2048 workgroups of 256 threads while keeping >= 8 clients per chunk
-    int64_t want = (2048 + bx - 1) / bx;
-    want = std::min<int64_t>(want, std::max<int64_t>(1, N / 8));
-    chunks = (int)std::max<int64_t>(1, want);
+    // 8 chunks (>= 8 clients each): at N = 1000-1250 every count from 8 to 16 measured within
+    // 5 % of the best and the earlier "~2048 workgroups" rule (74-103 chunks) 10-20 % slower
+    // (profiles/r05/agg_time.txt)
+    chunks = (int)std::max<int64_t>(1, std::min<int64_t>(8, N / 8));
   }
   if (chunks > N) chunks = N;
   // as many chunks as the workspace holds partials for (without one: a single chunk); an
@@ -119,4 +211,14 @@ extern "C" int fs_aggregate(const float* d_W_all, int64_t stride, const float* d
   }
   FS_LAUNCH_CHECK();
   return FS_OK;
+}
+
+}  // namespace fs
+
+using namespace fs;
+
+extern "C" int fs_aggregate(const float* d_W_all, int64_t stride, const float* d_p, int N, int64_t len,
+                            float* d_W_bar, float* d_ws, int64_t ws_floats, int chunks, void* stream) {
+  return aggregate_launch(d_W_all, stride, d_p, N, len, d_W_bar, d_ws, ws_floats, chunks, nullptr,
+                          reinterpret_cast<hipStream_t>(stream));
 }

@@ -13,6 +13,7 @@
 // sums go to a workspace and a one-block finalizer folds them in a fixed order, so the
 // result is bitwise reproducible run to run.  HBM-bound: one read of the test features.
 #include "common.h"
+#include "finalize.h"
 #include "eval_rows.h"
 
 namespace fs {
@@ -45,22 +46,7 @@ __global__ __launch_bounds__(EV_WAVES * 64) void eval_kernel(const float* __rest
 __global__ __launch_bounds__(256) void eval_finalize(const double* __restrict__ part, int nb, int n,
                                                     double* __restrict__ out) {
   __shared__ double s[2][256];
-  double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < nb; i += 256) { a += part[2 * i]; b += part[2 * i + 1]; }
-  s[0][threadIdx.x] = a;
-  s[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) {
-      s[0][threadIdx.x] += s[0][threadIdx.x + h];
-      s[1][threadIdx.x] += s[1][threadIdx.x + h];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    out[0] = s[0][0] / (double)n;
-    out[1] = 100.0 * s[1][0] / (double)n;
-  }
+  eval_finalize_block(part, nb, n, out, s);
 }
 
 int eval_finalize_launch(const double* part, int nb, int n, double* out, hipStream_t st) {

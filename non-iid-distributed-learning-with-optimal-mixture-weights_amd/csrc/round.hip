@@ -35,6 +35,7 @@
 #include <cstdio>
 
 #include "common.h"
+#include "finalize.h"
 #include "mt_replay.h"
 
 namespace fs {
@@ -131,6 +132,8 @@ struct fs_plan {
   int64_t max_client_steps = 0;       // E * ceil(max_j n_j / B)
   int fuse_E = 0;                     // evaluation blocks a TRAIN launch can carry (0: none)
   int eval_pending = -1;              // round whose evaluation rides on the next TRAIN launch
+  int fin_pending = -1;               // round whose fused evaluation awaits its finaliser (it rides
+                                      // on the next AGGREGATE launch, fs_plan_round)
   hipStream_t copy = nullptr;
   hipEvent_t uploaded[2] = {nullptr, nullptr};
   hipEvent_t consumed[2] = {nullptr, nullptr};
@@ -526,6 +529,15 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
   // a deferred evaluation rides on this TRAIN launch (it reads W_g before the launch
   // rewrites nothing but W_out); anything else that follows it runs it on its own first
   fs::FuseEval fuse{d.d_phi_t, d.d_labels_t, (int)d.n_t, p->fuse_E, d.d_eval_ws};
+  auto fin_of = [&](int te) { return fs::EvalFinalize{d.d_eval_ws, p->fuse_E, (int)d.n_t, d.d_eval_hist + 2 * (int64_t)te}; };
+  // a finaliser left by an earlier TRAIN call rides on this call's aggregation -- unless this
+  // call trains (its fused evaluation rewrites the partials) or does not aggregate: then first
+  if (p->fin_pending >= 0 && ((phases & FS_PHASE_TRAIN) || !(phases & FS_PHASE_AGGREGATE))) {
+    const fs::EvalFinalize f = fin_of(p->fin_pending);
+    p->fin_pending = -1;
+    const int rc = fs::eval_finalize_launch(f.part, f.nb, f.n, f.out, st);
+    if (rc != FS_OK) return rc;
+  }
   const bool fused = (phases & FS_PHASE_TRAIN) && p->eval_pending >= 0 && p->fuse_E > 0;
   if (p->eval_pending >= 0 && !fused) {
     const int rc = flush_eval(p, st);
@@ -575,19 +587,26 @@ extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const floa
     FS_HIP(hipEventRecord(p->consumed[s], st), "fs_plan_round");
     p->cons_recorded[s] = true;
   }
+  // the fused evaluation's finaliser rides on the next aggregation launch, this call's or a later
+  // call's (the two are independent: the partials of round t_eval's W_g vs this round's W_out;
+  // the FedAvg driver's TRAIN and AGGREGATE | EVAL calls of a round: one launch fewer per round)
   if (fused) {
     p->eval_pending = -1;
-    const int rc = fs::eval_finalize_launch(d.d_eval_ws, p->fuse_E, (int)d.n_t, d.d_eval_hist + 2 * (int64_t)t_eval, st);
-    if (rc != FS_OK) return rc;
+    p->fin_pending = t_eval;
   }
   if (phases & FS_PHASE_AGGREGATE) {
     const float* pw = d_p_override ? d_p_override : d.d_p;
     FS_REQUIRE(pw, "no mixture weights");
     const int64_t len = (int64_t)d.C * d.ld;
-    const int rc = fs_aggregate(d.d_W_out, len, pw, d.N, len, d.d_W_g, d.d_agg_ws, d.agg_ws_floats, d.agg_chunks,
-                                stream);
+    const fs::EvalFinalize fin = fin_of(p->fin_pending);
+    const bool with_fin = p->fin_pending >= 0;
+    p->fin_pending = -1;
+    const int rc = fs::aggregate_launch(d.d_W_out, len, pw, d.N, len, d.d_W_g, d.d_agg_ws, d.agg_ws_floats,
+                                        d.agg_chunks, with_fin ? &fin : nullptr, st);
     if (rc != FS_OK) return rc;
   }
+  // (a finaliser still pending here is launched by the next fs_plan_round call -- any call that
+  // trains or does not aggregate runs it first; results are read after such a call)
   if (phases & FS_PHASE_EVAL) {
     FS_REQUIRE(d.d_phi_t && d.d_labels_t && d.d_eval_hist && d.d_eval_ws, "no test set");
     if ((phases & FS_PHASE_EVAL_DEFER) && p->fuse_E > 0) {

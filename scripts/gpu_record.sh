@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
   || { echo "smoke rc=$?"; tail -30 gpurun_out/$R/smoke.log; exit 1; }
 tail -2 gpurun_out/$R/smoke.log
 for k in a b; do
-  timeout -k 10 400 python -u bench.py > gpurun_out/$R/bench_$k.json 2> gpurun_out/$R/bench_$k.err \
+  timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$R/bench_$k.json 2> gpurun_out/$R/bench_$k.err \
     || { echo "bench rc=$?"; tail -30 gpurun_out/$R/bench_$k.err; exit 1; }
   cut -c1-300 gpurun_out/$R/bench_$k.json
 done

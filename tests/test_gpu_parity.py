@@ -449,6 +449,32 @@ def test_aggregate_bitexact_and_chunked(amd):
     assert np.abs(out.cpu().numpy() - ref).max() <= 1e-6 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize('N', [1, 9, 15, 16, 37, 100, 300, 512, 513, 1250])
+def test_aggregate_auto_forms(amd, N):
+    """fs_aggregate with the shape's own choice (chunks = 0): one launch with in-workgroup
+    sub-range folds for 16 <= N <= 512 (round 5), the two-launch chunked fold above, and the
+    reference's exact single fold below 16 clients -- bitwise there; elsewhere only the order of
+    the N products' fp32 sum differs, so each element lies within the classical bound of two
+    recursive summations of the same terms, 2 (N - 1) u sum_j |p_j W_j| (u = 2^-24), of the
+    reference's fold."""
+    rs = np.random.RandomState(N)
+    C, D = 10, 2048
+    Ws = rs.normal(size=(N, C, D)).astype(np.float32)
+    p = rs.dirichlet(np.ones(N)).astype(np.float32)
+    ref = O.aggregate(list(Ws), p)
+    dev = torch.device('cuda')
+    agg = amd.engine.Aggregator(N, C, D, dev, chunks=0)
+    out = torch.full((C, D), float('nan'), device=dev)
+    agg.run(torch.from_numpy(Ws).to(dev), torch.from_numpy(p).to(dev), out)
+    got = out.cpu().numpy()
+    if N < 16:
+        np.testing.assert_array_equal(got, ref)
+    else:
+        S = np.abs(p.astype(np.float64)[:, None, None] * Ws).sum(0)
+        bound = 2.0 * (N - 1) * 2.0 ** -24 * S
+        assert (np.abs(got.astype(np.float64) - ref) <= bound).all(), np.max(np.abs(got - ref) / bound)
+
+
 def test_eval_unit_golden(amd):
     d = load('unit_test')
     dev = torch.device('cuda')
