@@ -960,19 +960,20 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
       for (int cand : {2, 4, 8, 16})
         if (split_fits(C, B, NT, cand) && cand <= cus) { G = cand; break; }
       // ... unless the pair form fits and its groups would walk several clients each (where it
-      // measured faster: config 3 5.16 vs 5.26 ms, config 4 0.434 vs 0.457 ms; with one client
-      // per group, config 2, the split form: 0.343 vs 0.366 ms -- profiles/r03/pair_ab.txt), or
-      // fs_tuning.train_form asks for it (1: never, 2: wherever it fits)
+      // measured faster: config 4 0.434 vs 0.457 ms; with one client per group, config 2, the
+      // split form: 0.343 vs 0.366 ms -- profiles/r03/pair_ab.txt) and there is no prox term
+      // (round 5, config 3: split G = 4 5.09-5.11 ms vs pair G = 8 5.24-5.26 and pipe G = 4
+      // 5.25-5.27, profiles/r05/forms_config3_4.txt; round 3 had measured the pair form ahead,
+      // 5.16 vs 5.26), or fs_tuning.train_form asks for it (1: never, 2: wherever it fits)
       const int form = tuning().train_form;
       if (form != 1)
         for (int cand : {2, 4, 8, 16})
           if (pair_fits(C, B, NT, cand) && cand <= cus &&
-              (form == 2 || G == 0 || (int64_t)N > (int64_t)split_groups(N, G, 0, cus))) {
+              (form == 2 || G == 0 || (!prox && (int64_t)N > (int64_t)split_groups(N, G, 0, cus)))) {
             *G_out = cand | FS_G_PAIR;
             *ws_bytes_out = pair_ws_bytes(N, cand, B, cus);
             return FS_OK;
           }
-      (void)prox;
     }
   }
   (void)max_en;

@@ -102,7 +102,9 @@ def test_pair_planner_and_train_form(amd):
     assert plan(1250, 10, 32, 2048, 0)[0] == 2 | amd.lib.G_PIPE      # config 4: the pipe form (ABI 14)
     with amd.lib.tuning(split_pipe=-1):
         assert plan(1250, 10, 32, 2048, 0)[0] == 4 | P               # ... the pair form without it
-    assert plan(1000, 7, 32, 4096, 0, prox=1)[0] == 8 | P            # config 3 (FedProx: the pair form)
+    assert plan(1000, 7, 32, 4096, 0, prox=1)[0] == 4                # config 3 (FedProx: the split form, r05)
+    with amd.lib.tuning(train_form=2):
+        assert plan(1000, 7, 32, 4096, 0, prox=1)[0] == 8 | P        # ... the pair form when asked for
     assert plan(1000, 7, 32, 4096, 0)[0] == 4 | amd.lib.G_PIPE       # ... its shape without the prox term
     assert plan(300, 10, 32, 1024, 0)[0] == 2 | P
     with amd.lib.tuning(train_form=2):
