@@ -98,7 +98,6 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 // width G / 2.
 template <int RT, int G, bool PROX, int EARLY, int TEAMS>
 __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
-  static_assert(EARLY == 0 || !PROX, "early row issue: the prox anchor's loads would queue behind it");
   static_assert(TEAMS == 1 || TEAMS == 2, "teams");
   constexpr int NW = SP_WAVES / TEAMS;             // waves per client lane
   constexpr int NTH = NW * 64;
@@ -486,6 +485,18 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       // always holds valid rows -- so the step is one straight path with one register
       // assignment for xf)
       constexpr int NE1 = SP_E1 < NE ? SP_E1 : NE, NE2 = SP_E1 + SP_E2 < NE ? SP_E1 + SP_E2 : NE;
+      // with a prox term (round 5) the anchor's whole slice goes out first, ahead of the early rows,
+      // so the update waits only for it (the late form re-reads it per tile inside the backward,
+      // behind that tile's predecessors' row loads); lanes of padding classes read class C - 1's
+      // row -- every load unconditional, as the rows
+      float4 avall[PROX && NE > 0 ? TPW : 1][4];
+      if constexpr (PROX && NE > 0) {
+        const float* ap = anc + (int64_t)min(l16, C - 1) * ld + 64 * t0 + 4 * lg;
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) avall[i][q] = ld4(ap + 64 * (w + NW * i) + 16 * q);
+      }
       if constexpr (NE > 0)
 #pragma unroll
         for (int f = 0; f < NE1; ++f) issue_row(f);
@@ -561,7 +572,10 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
         const int Tl = w + NW * i;
         if (decltype(FULL)::value || Tl < NTS) {
           float4 av[4];                            // prox anchor of this tile (issued first: the
-          if (PROX && l16 < C) {                   // update waits only for these, not the rows)
+          if constexpr (PROX && EAN > 0) {         // update waits only for these, not the rows)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) av[q] = avall[i][q];
+          } else if (PROX && l16 < C) {
             const float* ap = anc + wbase() + 64 * Tl;
 #pragma unroll
             for (int q = 0; q < 4; ++q) av[q] = ld4(ap + 16 * q);
@@ -773,15 +787,22 @@ static void launch_split_teams(const LTParams& P, const SplitWS& X, int grid, si
 
 template <int RT, int G>
 static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
-  // early row issue where every workgroup's slice is full (NT = G * 16 tiles) and no prox
-  // anchor is re-read (fs_tuning.split_early: 0 = by shape, -1 = never)
+  // early row issue where every workgroup's slice is full (NT = G * 16 tiles)
+  // (fs_tuning.split_early: 0 = by shape, -1 = never)
   // Depth per width (profiles/r03/split_early_ab2.txt, launch ms): at G = 2 (128 KB of rows per
   // CU per step) 4 early loads are fastest (config 2: 0.300-0.302 vs 0.304-0.307 with 6), at
   // G = 16 6 (config 5: 5.34-5.36 vs 5.58 with 4)
+  // With a prox term (round 5) the anchor's slice (8 loads per wave) goes out ahead of the early
+  // rows, and 2 early rows measured fastest (config 3, G = 4, launch us, profiles/r05/prox_early_depth.txt:
+  // late 5,102-5,107; early 1: 4,678-4,691, 2: 4,488-4,530, 3: 4,605-4,622, 4: 4,539-4,544, 6: 4,699-4,715,
+  // 8: 4,713-4,720)
   constexpr int EARLY_G = (G == 2 && SP_EARLY > 4) ? 4 : SP_EARLY;
+  constexpr int EARLY_PROX = SP_EARLY < 2 ? SP_EARLY : 2;
   const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
-  if (P.prox) launch_split_s<RT, G, true, 0, 1>(P, X, grid, lds, st);
-  else if (full && EARLY_G > 0 && tuning().split_early >= 0) launch_split_s<RT, G, false, EARLY_G, 1>(P, X, grid, lds, st);
+  const bool early = full && EARLY_G > 0 && tuning().split_early >= 0;
+  if (P.prox && early) launch_split_s<RT, G, true, EARLY_PROX, 1>(P, X, grid, lds, st);
+  else if (P.prox) launch_split_s<RT, G, true, 0, 1>(P, X, grid, lds, st);
+  else if (early) launch_split_s<RT, G, false, EARLY_G, 1>(P, X, grid, lds, st);
   else launch_split_s<RT, G, false, 0, 1>(P, X, grid, lds, st);
 }
 

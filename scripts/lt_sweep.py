@@ -37,7 +37,9 @@ def main():
     ap.add_argument('--prox', action='store_true')
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--reg', type=int, default=1, help='ridge term on (FedAMW local training) or off (FedAvg)')
+    ap.add_argument('--early', choices=['auto', 'off'], default='auto', help="fs_tuning.split_early (the split form's early row issue)")
     a = ap.parse_args()
+    fedamw_amd._lib.set_tuning(split_early={'auto': 0, 'off': -1}[a.early])
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
     dev = torch.device('cuda')

@@ -1,6 +1,6 @@
 """The split form's early row issue (csrc/local_train_split.hip, ABI 11 fs_tuning.split_early).
 
-On full slices without a prox anchor (FedAvg, FedAMW's local training) each wave issues the first
+On full slices (FedAvg, FedAMW's local training; since round 5 FedProx too) each wave issues the first
 SP_E1 of its next-step row loads right after the hand-off, so they stream through the softmax
 instead of waiting for the backward.  Only the time a load is issued moves: the weights and
 losses must be BITWISE those of the late form (split_early = -1), which is itself pinned to the
@@ -29,16 +29,19 @@ def _both(amd, Xs, ys, W0, args, seed, G):
 @pytest.mark.parametrize('G', [2, 4, 8, 16])
 @pytest.mark.parametrize('B', [32, 16])
 @pytest.mark.parametrize('chained', [False, True])
-def test_split_early_bitwise(amd, G, B, chained):
+@pytest.mark.parametrize('prox', [False, True])
+def test_split_early_bitwise(amd, G, B, chained, prox):
     """Early == late issue, bitwise, on full slices (D = 1024 G - 24: the last tile ragged, its
     padded columns stay 0), ridge on, ragged clients incl. tail batches of 1 and 7 rows and an
-    empty client; chained clients carry the weights (and the row stream) across clients."""
-    rs = np.random.RandomState(G + B + 31 * chained)
-    D, C, E = 1024 * G - 24, 10, 2
+    empty client; chained clients carry the weights (and the row stream) across clients.  With
+    the prox term (round 5) the early form loads the anchor's whole slice ahead of its early rows
+    (W_start, or in a chain the previous client's result)."""
+    rs = np.random.RandomState(G + B + 31 * chained + 7 * prox)
+    D, C, E = 1024 * G - 24, 7 if prox else 10, 2
     sizes = [65, 33, 0, 7, 96, 1, 40]
     Xs, ys = _rand_clients(rs, sizes, D, C)
     W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
-    args = (0.4, E, B, False, 0.0, True, 0.002, chained)
+    args = (0.4, E, B, prox, 0.05 if prox else 0.0, True, 0.002, chained)
     (We, le), (Wl, ll) = _both(amd, Xs, ys, W0, args, 5, G)
     assert np.array_equal(We, Wl), np.abs(We - Wl).max()
     assert np.array_equal(le, ll)
