@@ -93,6 +93,18 @@ __device__ __forceinline__ void pp_own(T& x) {
 #define PP_STAMP(k)
 #endif
 
+// Wave issue priority (round 5): each SIMD issues its older wave first, so the second wave of
+// every SIMD (waves 4-7) fell behind over a step and waves 0-3 waited at B1a (stamps, DESIGN.md
+// 4.1).  PP_PRIO bit 2: from each tile's barrier to the end of its hand-off (own sum, publish,
+// polls, image, softmax) a wave runs at priority 3, the MFMA phases at 0 -- the hand-off first
+// whichever wave holds it (config 2: 311-314 -> 300-302 us per launch; config 4: 427-430 ->
+// 421-427, profiles/r05/pipe_prio.txt); bit 1 (waves 4-7 at priority 1 throughout) measured no
+// gain.  -DPP_PRIO=m selects the experiment (scripts/build_pipe_prio_variant.sh).
+#ifndef PP_PRIO
+#define PP_PRIO 2
+#endif
+#define PP_SETPRIO(n) __builtin_amdgcn_s_setprio(n)
+
 __device__ __forceinline__ float invb_of(int bc) { return 1.0f / (float)bc; }
 
 template <int G, bool NRM, bool PROX>
@@ -188,6 +200,9 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
         for (int q = 0; q < 4; ++q)
           st4(Wj + base + 64 * (w + NW * i) + 16 * q, make_float4(wr[i][q][0], wr[i][q][1], wr[i][q][2], wr[i][q][3]));
   };
+  if (PP_PRIO & 1) {
+    if (w >= 4) PP_SETPRIO(1);                   // the SIMDs' second waves first
+  }
   const float nw0 = load_start();
   if (lane == 0) { wred[w][0] = 0.f; wred[w][1] = nw0; }
 
@@ -375,6 +390,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     forward(0);
     PP_STAMP(2)
     lds_barrier();                                  // B1a: wave partials of rt0 (and the norms)
+    if (PP_PRIO & 2) PP_SETPRIO(3);                 // the hand-off phases first
     PP_STAMP(3)
     const floatx4 own0 = own_sum(0);
     float nown[2] = {0.f, 0.f};
@@ -388,6 +404,10 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ================= row tile 1: forward (rt0's round trip runs under it), publish ========
     PP_STAMP(4)
+    if (PP_PRIO & 2) {
+      if ((PP_PRIO & 1) && w >= 4) PP_SETPRIO(1);
+      else PP_SETPRIO(0);
+    }
     pp_wait<W_F1>();                                // this step's rt1 rows landed
     PP_STAMP(5)
 #pragma unroll
@@ -397,6 +417,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     forward(1);
     PP_STAMP(6)
     lds_barrier();                                  // B1b
+    if (PP_PRIO & 2) PP_SETPRIO(3);
     PP_STAMP(7)
     const floatx4 own1 = own_sum(1);
     publish(1, own1);
@@ -582,6 +603,10 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
         }
       }
     };
+    if (PP_PRIO & 2) {
+      if ((PP_PRIO & 1) && w >= 4) PP_SETPRIO(1);
+      else PP_SETPRIO(0);
+    }
     take_g(0);
     PP_STAMP(12)
     bwd(0, 0);                                      // K0 (beside the other half's round trip)
