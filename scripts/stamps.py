@@ -32,6 +32,7 @@ def main():
     ap.add_argument('--pair', action='store_true', help='the pair form at width --G (or the planner\'s)')
     ap.add_argument('--teams', action='store_true', help='the team form at width --G (team 0 stamped)')
     ap.add_argument('--pipe', action='store_true', help='the pipe form at width --G')
+    ap.add_argument('--prox', action='store_true', help="FedProx's prox term (mu = 1e-3), ridge off")
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
     sh = SHAPES[a.config]
@@ -42,7 +43,7 @@ def main():
     feats = engine.Features(d['X_train'], d['y_train'], D, dev)
     L = fedamw_amd._lib
     split = (a.G | L.G_PAIR if a.pair else (a.G | L.G_TEAMS if a.teams else (a.G | L.G_PIPE if a.pipe else a.G))) or None
-    tr = engine.LocalTrainer(feats, C, B, E, split=split, chained=chained)
+    tr = engine.LocalTrainer(feats, C, B, E, split=split, chained=chained, prox=a.prox)
     names = PAIR_NAMES if tr.pair else (PIPE_NAMES if tr.pipe else NAMES)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     grid = 8 * tr.width if chained else tr.groups(cus) * tr.width
@@ -54,7 +55,7 @@ def main():
     tr.upload_perms(rng.draw_pass_seeds(N * E))
     W0 = torch.zeros(C, feats.ld, device=dev)
     for _ in range(3):
-        tr.run(W0, 0.5, False, 0, True, 1e-5, chained)
+        tr.run(W0, 0.5, a.prox, 1e-3, not a.prox, 1e-5, chained)
     torch.cuda.synchronize()
     tr.check_errors()
     st = tr.ws[base:base + extra].view(torch.int64).view(-1, 16).cpu().numpy().astype(np.float64)
