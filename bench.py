@@ -265,20 +265,34 @@ def load_record(tag, kernel):
     return rec, 'PMC %s' % rec.get('source', '')
 
 
-def settle_clocks(dev, ms):
-    """Hold the GPU busy for ``ms`` milliseconds of plain fp32 GEMMs and 1 GiB device copies (no
-    part of the workload: nothing of it is computed, cached or skipped) before a measurement's
-    warm-up rounds.  From idle the device takes tens of ms of sustained load to reach its
-    steady clocks: config 2 at the driver's --warmup 5 ran 0.311-0.317 ms per round, after 100 ms
-    of this settle 0.299-0.302, after 50 / 200 warm-up rounds of the workload itself 0.292 / 0.290
-    (profiles/r05/warmup_ab.txt) -- a 20-round timed region would otherwise measure part of the
-    clock ramp.  Reported on the line as ``device_settle_ms``; FS_BENCH_SETTLE_MS overrides the
-    length (0 = off), FS_BENCH_SETTLE_KIND = gemm | copy | mixed the load."""
+def settle_clocks(dev, ms, work=None):
+    """Hold the GPU busy for ``ms`` milliseconds before a measurement's warm-up rounds, so that a
+    short timed region does not measure the device's clock ramp.  From idle the device takes tens
+    of ms of sustained load to reach its steady clocks, and the steady state depends on the kind
+    of load: config 2 at the driver's --warmup 5 ran 0.311-0.317 ms per round from idle,
+    0.299-0.302 after 100 ms of fp32 GEMMs + 1 GiB copies, 0.292 / 0.290 after 50 / 200 warm-up
+    rounds of the workload itself (profiles/r05/warmup_ab.txt).  So by default (``work`` given,
+    FS_BENCH_SETTLE_KIND unset or 'workload') the settle repeats ``work`` -- launches of the
+    workload's own local-training kernel into a scratch trainer on the same features, with
+    shuffles from a private generator (the Federation's state and torch's global RNG are not
+    touched; nothing the timed rounds read is produced here) -- and otherwise plain GEMMs / copies
+    (FS_BENCH_SETTLE_KIND = gemm | copy | mixed).  Reported on the line as ``device_settle_ms``
+    and ``device_settle_kind``; FS_BENCH_SETTLE_MS overrides the length (0 = off).
+    Returns (ms, kind)."""
     ms = float(os.environ.get('FS_BENCH_SETTLE_MS', ms))
     if ms <= 0 or dev.type != 'cuda':
-        return 0.0
+        return 0.0, None
     import torch
-    kind = os.environ.get('FS_BENCH_SETTLE_KIND', 'mixed')           # GEMMs and 1 GiB copies
+    kind = os.environ.get('FS_BENCH_SETTLE_KIND', 'workload' if work is not None else 'mixed')
+    if kind == 'workload' and work is None:
+        kind = 'mixed'
+    if kind == 'workload':
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < ms:
+            work()
+            torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, kind
     a = torch.randn(4096, 4096, device=dev)
     b = torch.randn(4096, 4096, device=dev)
     x = torch.empty(256 << 20, dtype=torch.float32, device=dev)      # 1 GiB streamed
@@ -294,7 +308,30 @@ def settle_clocks(dev, ms):
             x.copy_(y)
         torch.cuda.synchronize()
     del x, y
-    return (time.perf_counter() - t0) * 1e3
+    return (time.perf_counter() - t0) * 1e3, kind
+
+
+def train_settle_work(fed, algo, lr):
+    """The settle's unit of work for ``fed``: one launch of fed's local-training kernel form (same
+    features, width and terms) into a scratch trainer, from a scratch copy of the global model,
+    with shuffles drawn from a private numpy generator.  Returns (work, release)."""
+    import torch
+    from fedamw_amd import engine
+    tr = engine.LocalTrainer(fed.feats, fed.C, fed.B, fed.E, split=fed.trainer.G, chained=False,
+                             prox=algo == 'fedprox')
+    seeds = np.random.default_rng(12345).integers(0, 2 ** 62, size=len(tr.pass_n), dtype=np.int64)
+    tr.upload_perms(seeds)
+    W0 = fed.W_g.detach().clone()
+    prox, reg = algo == 'fedprox', algo == 'fedamw'
+
+    def work():
+        tr.run(W0, lr, prox, 5e-4 if prox else 0.0, reg, 1e-5, False)
+
+    def release():
+        nonlocal tr
+        tr = None
+        torch.cuda.synchronize()
+    return work, release
 
 
 def phase_ms(events, name):
@@ -468,7 +505,7 @@ def config1_leg(dev, rounds=10, warmup=2, cpu_budget=3.0):
     fed = tools.Federation('fedamw', d['X_train'], d['y_train'], d['X_test'], d['y_test'], d['validloader'],
                            'classification', C, D, lr, E, B, False, 0.0, True, lam, R, lr_p, 'sequential',
                            verbose=False)
-    settled = settle_clocks(dev, 100.0)
+    settled, settle_kind = settle_clocks(dev, 100.0)
     for _ in range(warmup):
         fed.round()
     torch.cuda.synchronize()
@@ -583,7 +620,10 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                            E, B, algo == 'fedprox', mu, fedamw, 1e-5, R, 1e-3,
                            'parallel', verbose=False, shuffle_device=not host_shuffle)
     assert len(fed.mine) == N_loc
-    settled = settle_clocks(dev, 100.0)
+    work, release = train_settle_work(fed, algo, lr)
+    settled, settle_kind = settle_clocks(dev, 100.0, work)
+    release()
+    del work, release
     for _ in range(warmup):
         fed.round()
     torch.cuda.synchronize()
@@ -638,6 +678,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                                                                ('split' if fed.trainer.G > 1 else 'single')))},
         'final_test_acc': float(ta[fed.t - 1]),
         'device_settle_ms': settled,
+        'device_settle_kind': settle_kind,
     }
     if fedamw:
         nv = fed.mixture.nv
@@ -717,6 +758,7 @@ def worker(args):
         'roofline': main['roofline'],
         'final_test_acc': main['final_test_acc'],
         'device_settle_ms': main['device_settle_ms'],
+        'device_settle_kind': main['device_settle_kind'],
     }
     for k in ('fedamw', 'cpu_baseline'):
         if k in main:
@@ -730,7 +772,8 @@ def worker(args):
             obj = {'workload': r['workload'], 'value': r['value'], 'unit': 'client-rounds/s',
                    'ms_per_round': r['ms_per_step'], 'rounds_timed': k, 'warmup': w, 'scaling': r['scaling'],
                    'roofline': r['roofline'], 'final_test_acc': r['final_test_acc'],
-                   'device_settle_ms': r['device_settle_ms'], 'leg_wall_s': time.perf_counter() - t0}
+                   'device_settle_ms': r['device_settle_ms'], 'device_settle_kind': r['device_settle_kind'],
+                   'leg_wall_s': time.perf_counter() - t0}
             for key in ('fedamw', 'cpu_baseline'):
                 if key in r:
                     obj[key] = r[key]
