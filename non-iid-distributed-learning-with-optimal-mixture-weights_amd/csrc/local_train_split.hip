@@ -43,7 +43,6 @@
 namespace fs {
 
 constexpr int SP_WAVES = 8;
-constexpr int SP_THREADS = SP_WAVES * 64;
 constexpr int SP_TPW = 2;                 // max 64-column tiles per wave (register budget)
 constexpr unsigned SP_SPIN_LIMIT = 1u << 22;
 constexpr int SP_ERR_BYTES = 256;         // error block at the END of the workspace (never memset)
@@ -96,15 +95,23 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 // run beside the other team's MFMAs.  Per wave the work is the split form's at 4 waves per
 // slice (TPW = 2 tiles), so a team form at width G holds the registers of the split form at
 // width G / 2.
-template <int RT, int G, bool PROX, int EARLY, int TEAMS>
-__global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
+// WAVES / TPWK (round 5): waves per workgroup and tiles per wave.  The shipped forms are 8 waves
+// of up to 2 tiles; the NARROW chained instances (exp.py's config 1: D = 2000 -> 32 tiles) give
+// every wave exactly one tile -- 4 waves at G = 8 (4 tiles per slice), 8 waves at G = 4 -- so the
+// slice is full and the step runs the early row issue with no per-tile guard.  (The 8-wave form
+// at 4 tiles per slice left waves 4-7 without a tile and guarded tile 1 of every wave: the
+// compiler then waited vmcnt(0) for the whole next-step row stream at that guard's join, inside
+// the backward -- 5.4 k of config 1's 12.1 k cycles per step, profiles/r05b/stamps_c1.txt.)
+template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
+__global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   static_assert(TEAMS == 1 || TEAMS == 2, "teams");
-  constexpr int NW = SP_WAVES / TEAMS;             // waves per client lane
+  static_assert(WAVES == SP_WAVES || (WAVES == 4 && TEAMS == 1), "waves");
+  constexpr int NW = WAVES / TEAMS;                // waves per client lane
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
-  constexpr int TPW = SP_TPW;
+  constexpr int TPW = TPWK;
   constexpr int XT = NTH;                         // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
   constexpr int M = ((G >= 8 ? 512 : NZ + 2) + XT - 1) / XT;
@@ -147,7 +154,8 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
   // idle, LDS from the (unused) image
   const int nb = gridDim.x - P.fuse_E;
   if ((int)blockIdx.x >= nb) {
-    eval_persistent<SP_WAVES>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
+    if constexpr (WAVES == SP_WAVES)
+      eval_persistent<SP_WAVES>(P.fuse_phi, P.ld, P.fuse_y, P.fuse_n, P.W_start, P.C, (int)blockIdx.x - nb, P.fuse_E,
                          xs_dyn, P.fuse_part);
     return;
   }
@@ -484,7 +492,9 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
       // (EARLY instances run only on full slices and issue every load unconditionally -- pn
       // always holds valid rows -- so the step is one straight path with one register
       // assignment for xf)
-      constexpr int NE1 = SP_E1 < NE ? SP_E1 : NE, NE2 = SP_E1 + SP_E2 < NE ? SP_E1 + SP_E2 : NE;
+      // (one tile per wave, the narrow chained instances: the whole step's rows go out at once)
+      constexpr int E1 = TPW == 1 ? NE : SP_E1;
+      constexpr int NE1 = E1 < NE ? E1 : NE, NE2 = E1 + SP_E2 < NE ? E1 + SP_E2 : NE;
       // with a prox term (round 5) the anchor's whole slice goes out first, ahead of the early rows,
       // so the update waits only for it (the late form re-reads it per tile inside the backward,
       // behind that tile's predecessors' row loads); lanes of padding classes read class C - 1's
@@ -591,9 +601,17 @@ __global__ __launch_bounds__(SP_THREADS, 1) void local_train_split_kernel(LTPara
           const int RSx = decltype(FULL)::value ? RS_FULL : RS;
           const float* ib0 = xs_lds + lg * RSx + 64 * Tl + 4 * (rblk ^ lg);
           const float* ib1 = xs_lds + lg * RSx + 64 * Tl + 4 * (rblk ^ (lg + 4));
+          // one tile per wave (narrow, one wave per SIMD at 4 waves): nothing hides an image
+          // read's latency behind another wave's MFMAs, so the tile's reads all go out first
+          float4 xpre[TPW == 1 ? 4 * RT : 1];
+          if constexpr (TPW == 1) {
+#pragma unroll
+            for (int kk = 0; kk < 4 * RT; ++kk) xpre[kk] = ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RSx);
+            __builtin_amdgcn_sched_barrier(0);
+          }
 #pragma unroll
           for (int kk = 0; kk < 4 * RT; ++kk) {
-            const float4 x = ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RSx);
+            const float4 x = TPW == 1 ? xpre[kk] : ld4(((kk & 1) ? ib1 : ib0) + 4 * kk * RSx);
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4) ga[e4] = mfma4(comp(x, e4), gB[kk], ga[e4]);
             if constexpr (decltype(LD)::value) {
@@ -766,13 +784,41 @@ static unsigned split_spin_limit() {
 }
 unsigned split_spin_bound() { return split_spin_limit(); }
 
-template <int RT, int G, bool PROX, int EARLY, int TEAMS>
+template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY, TEAMS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY, TEAMS>), dim3(grid), dim3(SP_THREADS), lds, st, P,
-                     X);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK>), dim3(grid), dim3(WAVES * 64),
+                     lds, st, P, X);
+}
+
+// the narrow chained instances (one tile per wave, full slices, every row load early): NT = 4 G
+// on 4-wave workgroups, NT = 8 G on 8-wave ones.  A 4-wave workgroup asks for 96 KB of LDS so
+// that no two share a CU.  (fs_tuning.split_early = -1 turns them off with the early issue: the
+// chain then runs the late 8-wave form, bitwise the same weights.)
+constexpr int SPLIT_NARROW_EARLY = 8;
+template <int RT, int G>
+static bool launch_split_narrow(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if constexpr (RT != 2 || G < 4) {
+    return false;
+  } else {
+    const int64_t NT = P.ld >> 6;
+    if (!P.chained || P.fuse_E > 0 || tuning().split_early < 0) return false;
+    if (NT == 4 * G) {
+      const size_t l4 = std::max(lds, (size_t)96 * 1024);
+      if (P.prox) launch_split_s<RT, G, true, SPLIT_NARROW_EARLY, 1, 4, 1>(P, X, grid, l4, st);
+      else launch_split_s<RT, G, false, SPLIT_NARROW_EARLY, 1, 4, 1>(P, X, grid, l4, st);
+      return true;
+    }
+    if (NT == 8 * G) {
+      if (P.prox) launch_split_s<RT, G, true, SPLIT_NARROW_EARLY, 1, SP_WAVES, 1>(P, X, grid, lds, st);
+      else launch_split_s<RT, G, false, SPLIT_NARROW_EARLY, 1, SP_WAVES, 1>(P, X, grid, lds, st);
+      return true;
+    }
+    return false;
+  }
 }
 
 // the team form (G | FS_G_TEAMS): parallel clients, G = 4 or 8 (config 2 / 3 / 4 widths)
@@ -800,6 +846,7 @@ static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t
   constexpr int EARLY_PROX = SP_EARLY < 2 ? SP_EARLY : 2;
   const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
   const bool early = full && EARLY_G > 0 && tuning().split_early >= 0;
+  if (launch_split_narrow<RT, G>(P, X, grid, lds, st)) return;
   if (P.prox && early) launch_split_s<RT, G, true, EARLY_PROX, 1>(P, X, grid, lds, st);
   else if (P.prox) launch_split_s<RT, G, true, 0, 1>(P, X, grid, lds, st);
   else if (early) launch_split_s<RT, G, false, EARLY_G, 1>(P, X, grid, lds, st);

@@ -67,3 +67,23 @@ def test_split_early_persistent_groups_vs_oracle(amd):
             assert abs(le[j] - lref) <= 2e-5 * max(1.0, abs(lref)), j
         else:
             torch.empty(2 * E, dtype=torch.int64).random_()     # the oracle's draws for client j
+
+
+@pytest.mark.parametrize('G', [4, 8, 16])
+@pytest.mark.parametrize('per', [4, 8])
+@pytest.mark.parametrize('prox', [False, True])
+def test_split_narrow_chained_bitwise(amd, G, per, prox):
+    """The narrow chained instances (round 5, session 2): slices of exactly ``per`` tiles, one tile
+    per wave -- 4-wave workgroups at 4 tiles (exp.py's config 1: D = 2000 at G = 8), 8 waves at 8
+    -- with every next-step row load early.  Same weights, bitwise, as the late 8-wave form
+    (split_early = -1), whose waves 4-7 hold no tile at 4 tiles per slice; the losses too, up to the
+    order of the cross-entropy partials (4 waves sum 2 rows each where 8 sum one)."""
+    rs = np.random.RandomState(7 * G + per + 3 * prox)
+    D, C, E, B = 64 * per * G - 24, 7 if prox else 2, 2, 32
+    sizes = [65, 33, 0, 7, 96, 1, 40]
+    Xs, ys = _rand_clients(rs, sizes, D, C)
+    W0 = (rs.normal(size=(C, D)) * 0.1).astype(np.float32)
+    args = (0.4, E, B, prox, 0.05 if prox else 0.0, True, 0.002, True)
+    (We, le), (Wl, ll) = _both(amd, Xs, ys, W0, args, 11, G)
+    assert np.array_equal(We, Wl), np.abs(We - Wl).max()
+    assert np.allclose(le, ll, rtol=1e-6, atol=0), np.abs(le - ll).max()
