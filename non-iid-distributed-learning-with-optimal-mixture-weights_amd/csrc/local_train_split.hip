@@ -261,15 +261,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   int pn[RT], lb[RT];
   SpCur lc;
   bool lc_ok = sp_seek(lc, P, grp, ng, T, 0);
-  auto fetch_rows = [&]() {
+  // the step's local row indices (raw) and its client's first row (base): pn = base + raw.
+  // (The add is left to the caller, so that issuing the loads does not wait for them.)
+  auto fetch_raw = [&](int* raw, int64_t& base) {
     const int e_ = lc.st / lc.nbat, s_ = lc.st - e_ * lc.nbat;
     const int b0_ = s_ * B, bc_ = min(B, lc.n - b0_);
     const int32_t* pp_ = P.perms + (int64_t)E * lc.row0 + (int64_t)e_ * lc.n + b0_;
+    base = lc.row0;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int r_ = rt * 16 + l16;
-      pn[rt] = (int)(lc.row0 + pp_[r_ < bc_ ? r_ : 0]);
+      raw[rt] = pp_[r_ < bc_ ? r_ : 0];
     }
+  };
+  auto fetch_rows = [&]() {
+    int raw[RT];
+    int64_t base;
+    fetch_raw(raw, base);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) pn[rt] = (int)(base + raw[rt]);
   };
 #define SP_XLOAD()                                                                   \
   {                                                                                  \
@@ -328,6 +338,31 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #ifdef FS_STAMPS
   unsigned long long stamp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_prev = 0;
 #endif
+  // the forward partial z_g = X_slice W_slice^T, tile by tile, into acc (RT row tiles)
+  floatx4 acc[RT];
+  auto fwd_tile = [&](int i) {
+    if (w + NW * i < NTS)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 xa[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) xa[rt] = xf[i][rt][q];
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xa[rt], e4), comp(wr[i][q], e4), acc[rt]);
+      }
+  };
+  auto fwd_tile0 = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    fwd_tile(0);
+  };
+  // pre: the step's tile-0 forward ran at the end of the previous step (round 5, session 2).  A
+  // step ends by waiting for its whole next-step row stream (hipcc drains vmcnt at the loop's
+  // back-edge); tile 0's rows are the stream's first half, so its MFMAs run there, in the
+  // stream's tail, instead of after it.  Same MFMAs in the same order: the same bits.
+  bool pre = false;
   for (; cc_ok; ++gs) {
     const int st = cc.st, n = cc.n, nbat = cc.nbat;
     if (st == 0) {
@@ -351,6 +386,30 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       if (w == 0 && lg == 0)
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) lab[par][rt * 16 + l16] = lb[rt];
+      // (round 5, session 2) the next step's labels and the row indices of the step after it
+      // are loaded here, ahead of this step's row stream: loaded after it (as before), the
+      // index arithmetic at the step's end waited vmcnt(0) for the whole next-step stream, so
+      // no part of the next forward could start on rows that had already landed
+      const bool ilv = lc_ok;
+      int lbn[RT], pnr[RT];
+      int64_t pnb = 0;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { lbn[rt] = lb[rt]; pnr[rt] = 0; }
+      bool lcn_ok = false;
+      // (the narrow chained instances keep the fetch at the step's end: their step is the hand-off
+      // chain, and these loads ahead of its polls cost more than the stream's tail -- config 1
+      // 7.0 vs 7.6 ms per launch, profiles/r05b/prefwd_forms.txt)
+      constexpr bool TOP_FETCH = TPW > 1;
+      auto fetch_next = [&]() {
+        if (ilv) {
+          if (w == 0 && lg == 0)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) lbn[rt] = P.labels[pn[rt]];
+          lcn_ok = sp_advance(lc, P, grp, ng, T);
+          if (lcn_ok) fetch_raw(pnr, pnb);
+        }
+      };
+      if constexpr (TOP_FETCH) fetch_next();
 
       // image write: the backward of this step reads the slice from LDS (each wave only ever
       // touches the image of its own tiles)
@@ -364,23 +423,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   }
 
       // ---------------- forward partial: z_g = X_slice W_slice^T ----------------
-      floatx4 acc[RT];
+      // (tile 0's part may already have run at the end of the previous step: `pre`)
+      if (!pre) fwd_tile0();
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < TPW; ++i)
-        if (w + NW * i < NTS)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float4 xa[RT];
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-              xa[rt] = xf[i][rt][q];
-#pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
-#pragma unroll
-              for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xa[rt], e4), comp(wr[i][q], e4), acc[rt]);
-          }
+      for (int i = 1; i < TPW; ++i) fwd_tile(i);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
         st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
@@ -570,7 +616,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       const int rblk = 4 * (l16 & 3) + (l16 >> 2);
       float npn = 0.f, nwn = 0.f;
       // this wave's next rows go out one load per backward iteration
-      const bool ilv = lc_ok;
       // (two instances, so the interleaved loads are straight-line code: a branch around each
       // load would make the compiler wait for it at the join)
       // FULL: every wave owns TPW tiles (NTS = NW * TPW, every BASELINE shape but chained config
@@ -656,12 +701,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       } else {
         bwd(std::false_type{}, std::false_type{}, E0{});
       }
+      if constexpr (!TOP_FETCH) fetch_next();
       if (ilv) {
-        if (w == 0 && lg == 0)                     // (after the rows: nothing waits on it here)
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) lb[rt] = P.labels[pn[rt]];
-        lc_ok = sp_advance(lc, P, grp, ng, T);
-        if (lc_ok) fetch_rows();
+        for (int rt = 0; rt < RT; ++rt) {
+          lb[rt] = lbn[rt];
+          if (lcn_ok) pn[rt] = (int)(pnb + pnr[rt]);
+        }
+        lc_ok = lcn_ok;
       }
       // the norms of the updated slice feed only the prox / ridge terms (loss and gradient): without
       // either nothing reads them; ridge alone sums ||W||^2 here in the update's own order (i, q,
@@ -679,6 +726,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         nwn = wave_sum_dpp(nwn, lane);
         if (lane == 0) { wred[w][0] = npn; wred[w][1] = nwn; }
       }
+      // the next step's tile-0 forward, where the next step continues this client (the weights
+      // stay; a new parallel client restarts from W_start at the step's top)
+      pre = TEAMS == 1 && TPW > 1 && st + 1 < cc.steps;
+      if (pre) fwd_tile0();
       SP_STAMP(8)
     }
     if (st == cc.steps - 1) {                     // client end
