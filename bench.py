@@ -312,12 +312,16 @@ def settle_clocks(dev, ms, work=None):
 
 
 def train_settle_work(fed, algo, lr):
-    """The settle's unit of work for ``fed``: one launch of fed's local-training kernel form (same
-    features, width and terms) into a scratch trainer, from a scratch copy of the global model,
-    with shuffles drawn from a private numpy generator.  Returns (work, release)."""
+    """The settle's unit of work for ``fed``: one launch of fed's local training (same features,
+    group width and terms) into a scratch trainer, from a scratch copy of the global model, with
+    shuffles drawn from a private numpy generator.  It runs the split form's LATE-issue instance
+    (fs_tuning.split_early = -1; the pipe width as a plain split group): the same work and load as
+    the timed launches under another kernel symbol, so that a kernel trace's statistics of the
+    timed form hold only the timed rounds' launches (with their deferred evaluation) and agree
+    with the line's launch time.  Returns (work, release)."""
     import torch
-    from fedamw_amd import engine
-    tr = engine.LocalTrainer(fed.feats, fed.C, fed.B, fed.E, split=fed.trainer.G, chained=False,
+    from fedamw_amd import _lib, engine
+    tr = engine.LocalTrainer(fed.feats, fed.C, fed.B, fed.E, split=fed.trainer.width, chained=False,
                              prox=algo == 'fedprox')
     seeds = np.random.default_rng(12345).integers(0, 2 ** 62, size=len(tr.pass_n), dtype=np.int64)
     tr.upload_perms(seeds)
@@ -325,7 +329,8 @@ def train_settle_work(fed, algo, lr):
     prox, reg = algo == 'fedprox', algo == 'fedamw'
 
     def work():
-        tr.run(W0, lr, prox, 5e-4 if prox else 0.0, reg, 1e-5, False)
+        with _lib.tuning(split_early=-1):
+            tr.run(W0, lr, prox, 5e-4 if prox else 0.0, reg, 1e-5, False)
 
     def release():
         nonlocal tr

@@ -4,6 +4,10 @@
 # Output: gpurun_out/pmc_<tag>/p<i>/...counter_collection.csv  (summarised by scripts/pmc_summary.py)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
+# the bench's device settle as GEMMs / copies here: its default (the workload's training kernel,
+# late-issue instance) would add settle launches to the captured kernels; counters are per launch,
+# so the settle's kind changes nothing the capture reports
+export FS_BENCH_SETTLE_KIND=mixed
 TAG=$1; ARGS=$2; REGEX=$3
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
