@@ -80,7 +80,10 @@ const char* fs_last_error(void);
  *   split_early        (ABI 11) split form without a prox anchor on full slices: 0 = issue the
  *                      first SP_E1 (local_train_split.hip: 4 at G = 2, 6 at G >= 4) of each
  *                      wave's 16 next-step row loads right after the hand-off (they stream
- *                      through the softmax), -1 = all of them inside the backward
+ *                      through the softmax), -1 = all of them inside the backward; since
+ *                      round 5 it covers the prox term (anchor slice first, 2 early rows) and
+ *                      the narrow chained instances (one tile per wave at 4 or 8 tiles per
+ *                      slice: every row load early); -1 turns both off (bitwise the same W)
  *   mix_qmc_lane_clients (ABI 13) qmc p-solver: clients per lane, 0 = by shape (4 where
  *                      K = ceil(N / 64) <= 16 workgroups, else 8 for C <= 10), 4 = force 4,
  *                      8 = force 8 where C <= 10 (K = ceil(N / 128)); same p to fp32 rounding
