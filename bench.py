@@ -77,6 +77,9 @@ LEGS = ((4, 10, 10), (3, 5, 2), (5, 2, 1))     # (config, timed rounds, warm-up 
 # the box's 16 host threads, so its baseline is a measured round instead of an extrapolation
 # (VERDICT round 4, weak item 4); config 5's (~1 min of CPU per round) stays a stated sample
 LEG_CPU_SECONDS = {3: 6.0}
+# FedAMW legs whose CPU baseline is one whole oracle round timed end to end when the sample's
+# estimate is at most this many seconds (config 5: ~90 s on 16 host cores)
+CPU_WHOLE_ROUND_MAX_S = {5: 150.0}
 
 
 def parse(argv=None):
@@ -105,9 +108,10 @@ def parse(argv=None):
     ap.add_argument('--train-form', choices=['auto', 'split', 'pair', 'teams', 'pipe'], default='auto',
                     help="fs_tuning.train_form / split_teams / split_pipe: the local-training kernel form for parallel "
                          "clients (A/B runs)")
-    ap.add_argument('--launch-timeout', type=float, default=0.0,
-                    help='--gpus N launcher: wall-clock bound on the whole run (seconds; default 0 = none: a '
-                         'long but healthy run is never cut; exit code 124 when it trips)')
+    ap.add_argument('--launch-timeout', type=float, default=None,
+                    help='--gpus N launcher: wall-clock bound on the whole run (seconds; default 1800 + 10 s per '
+                         'timed or warm-up round + 60 s per FedAMW round, so a long but healthy run is not cut and a '
+                         'launch whose every rank hangs still ends; 0 = none; exit code 124 when it trips)')
     ap.add_argument('--teardown-timeout', type=float, default=300.0,
                     help='--gpus N launcher: once a worker has exited 0, the seconds the others get to finish '
                          '(a rank hung in a collective or in teardown); exit code 124 when it trips (0 = none)')
@@ -122,7 +126,16 @@ def parse(argv=None):
     a.custom = any(getattr(a, k) != v for k, v in PRESETS[a.config].items() if k != 'algo')
     if a.rounds is None:
         a.rounds = 100
+    if a.launch_timeout is None:
+        a.launch_timeout = default_launch_timeout(a)
     return a
+
+
+def default_launch_timeout(a):
+    """The launcher's default whole-run bound (with no bound, a launch whose
+    every rank hangs in a collective before any finishes would wait forever): generous, and
+    scaled to the work asked for."""
+    return 1800.0 + 10.0 * (a.steps + a.warmup) + 60.0 * a.fedamw_rounds
 
 
 # --------------------------------------------------------------------------------------------
@@ -142,9 +155,9 @@ def spawn(n, cmd=None, timeout=None, teardown=None):
     exited 0.  A failed worker ends the others (they would wait forever in a collective).
     Two wall-clock bounds, each ending the workers (terminate, then kill) with exit code 124:
     ``teardown`` (default --teardown-timeout, 300 s) counts from the first worker that exits 0
-    -- a rank hung in a collective or in teardown after the others finished must not hold the
-    launcher forever -- and ``timeout`` (default --launch-timeout: none) bounds the whole run,
-    so a long but healthy run (large --steps, --fedamw-rounds) is never cut by default."""
+    or from rank 0's result line, whichever comes first -- a rank hung in a collective or in
+    teardown after the result is out must not hold the launcher forever -- and ``timeout``
+    (default --launch-timeout: 1800 s + a per-round allowance) bounds the whole run."""
     if timeout is None or teardown is None:
         a = parse() if cmd is None else None
         if timeout is None:
@@ -161,10 +174,14 @@ def spawn(n, cmd=None, timeout=None, teardown=None):
         env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
 
+    line_out = []                        # time rank 0's JSON result line was relayed
+
     def relay(pipe):
         for line in pipe:
             sys.stdout.write(line)
             sys.stdout.flush()
+            if line.lstrip().startswith('{') and not line_out:
+                line_out.append(time.time())
 
     th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
     th.start()
@@ -190,8 +207,8 @@ def spawn(n, cmd=None, timeout=None, teardown=None):
             stop_all()
             break
         now = time.time()
-        if t_first_done is None and any(p.poll() == 0 for p in procs):
-            t_first_done = now
+        if t_first_done is None and (line_out or any(p.poll() == 0 for p in procs)):
+            t_first_done = line_out[0] if line_out else now
         late = ('launch', timeout) if timeout and now - t_start > timeout else (
             ('teardown', teardown) if teardown and t_first_done is not None and now - t_first_done > teardown else None)
         if late:
@@ -348,7 +365,39 @@ def _np(x):
     return x.detach().cpu().numpy()
 
 
-def cpu_baseline(d, wl, budget, fedamw, rounds_R, z_rows=None):
+def cpu_fedamw_round(d, wl, rounds_R, lr_p=1e-3):
+    """One WHOLE FedAMW round of the numpy oracle, timed end to end (config
+    5's CPU baseline measured, not extrapolated): the local training of all N clients
+    (tools.py:430-434), the Z GEMM of every client model on every validation row (448, hoisted), the
+    R inner epochs of p-SGD over the pooled validation set (441-453), the aggregate with the learned
+    p (455-460) and the test evaluation (461).  Returns (seconds, sample text)."""
+    from oracle import fedsim_oracle as O
+    N, D, C = len(d['X_train']), wl['D'], wl['C']
+    W = O.mlp_init(D, C)
+    Xv, yv = _np(d['X_val']).astype(np.float32), _np(d['y_val']).astype(np.int64)
+    Xt, yt = _np(d['X_test']), _np(d['y_test'])
+    t0 = time.perf_counter()
+    Ws = [O.train_client(_np(d['X_train'][j]), _np(d['y_train'][j]), W, 0.5, 2, 32, False, 0.0, True, 1e-5)[0]
+          for j in range(N)]
+    t_train = time.perf_counter() - t0
+    a = time.perf_counter()
+    Z = np.einsum('ncd,vd->ncv', np.stack(Ws).astype(np.float32), Xv, optimize=True)
+    t_z = time.perf_counter() - a
+    a = time.perf_counter()
+    p, _ = O.mixture_solve_z(Z, yv, np.full(N, 1.0 / N, np.float32), None, lr_p, rounds_R, 16)
+    t_solve = time.perf_counter() - a
+    del Z
+    O.test_eval(Xt, yt, O.aggregate(Ws, p))
+    el = time.perf_counter() - t0
+    nv = len(yv)
+    return el, ('1 whole FedAMW round of the numpy oracle timed end to end: %d client trainings (%d rows, D=%d, '
+                'C=%d, E=2, B=32; %.1f s), the Z GEMM on all %d validation rows (%.1f s), all %d p-SGD steps '
+                '(%d passes; %.1f s), aggregate + %d-row test eval; %.1f s'
+                % (N, len(d['y_train'][0]), D, C, t_train, nv, t_z, rounds_R * ((nv + 15) // 16), rounds_R, t_solve,
+                   len(yt), el))
+
+
+def cpu_baseline(d, wl, budget, fedamw, rounds_R, z_rows=None, whole_max_s=0.0):
     """The numpy oracle on this host's cores, on a bounded sample of the same workload:
     local training of as many clients as fit ~60 % of ``budget`` (whole rounds when they all
     fit), the aggregate and the test evaluation; FedAMW adds the Z GEMM on a sample of the
@@ -420,9 +469,16 @@ def cpu_baseline(d, wl, budget, fedamw, rounds_R, z_rows=None):
         sample += ('; FedAMW: Z GEMM on %d of %d validation rows, %d of the round\'s %d p-SGD steps on %s (N=%d)'
                    % (sv, nv, ps, steps, zsrc, N))
     el = time.perf_counter() - t0
-    torch.set_rng_state(state)
     threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
     whole = bool(rounds) and not fedamw
+    if fedamw and whole_max_s > 0 and t_round <= whole_max_s:
+        # the sample's estimate fits: time one whole round instead (measured, factor 1)
+        sec, text = cpu_fedamw_round(d, wl, rounds_R)
+        torch.set_rng_state(state)
+        return {'value': N / sec, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
+                'measured': True, 'extrapolation_factor': 1.0, 'sample': text,
+                'sample_estimate': N / t_round}
+    torch.set_rng_state(state)
     return {'value': N / t_round, 'unit': 'client-rounds/s', 'cores': int(threads), 'kind': 'port',
             'measured': whole, 'extrapolation_factor': 1.0 if whole else t_round / el,
             'sample': sample + ' of the numpy oracle, %.1f s, %s' % (
@@ -651,6 +707,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
         el = float(t.item())
     lt_ms = phase_ms(fed.events, 'train')
     tr, tl, ta = fed.results()
+    agg = aggregate_timing(fed, wl)
     n_rows = int(fed.feats.rows)
     alg_bytes = 4.0 * E * n_rows * wl['D'] + 8.0 * E * n_rows + 8.0 * N_loc * wl['C'] * wl['D']
     achieved = alg_bytes / (lt_ms * 1e-3) / 1e9 if lt_ms else float('nan')
@@ -681,6 +738,7 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
                      'form': 'pair' if fed.trainer.pair else ('teams' if fed.trainer.teams else
                                                               ('pipe' if fed.trainer.pipe else
                                                                ('split' if fed.trainer.G > 1 else 'single')))},
+        'aggregate': agg,
         'final_test_acc': float(ta[fed.t - 1]),
         'device_settle_ms': settled,
         'device_settle_kind': settle_kind,
@@ -710,11 +768,45 @@ def run_workload(wl, ws, rank, dev, steps, warmup, R_arg, cpu_seconds, host_shuf
         if fedamw:                      # the round's own Z rows (all clients) for the p-SGD sample
             mx = fed.mixture
             z_rows = _np(mx.Z[:512].view(-1, wl['C'], mx.ldN)[:, :, :mx.N].permute(2, 1, 0))
-        out['cpu_baseline'] = cpu_baseline(d, wl, cpu_seconds, fedamw, R_arg, z_rows)
+        out['cpu_baseline'] = cpu_baseline(d, wl, cpu_seconds, fedamw, R_arg, z_rows,
+                                           whole_max_s=CPU_WHOLE_ROUND_MAX_S.get(cfg, 0.0) if not custom else 0.0)
     del fed, d, Xs, ys, vl
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
+
+
+def aggregate_timing(fed, wl, reps=20):
+    """fs_aggregate -- the weighted aggregation kernel of the round (tools.py:345-350, 455-460) --
+    timed with HIP events after the timed rounds: the round's own launch
+    (FedAvg / FedProx: the plan's AGGREGATE phase; FedAMW: the Aggregator with the learned p) on
+    the round's own clients x params buffer, ``reps`` launches back to back, the mean per launch.
+    Algorithmic bytes per launch = 4 N C D (the clients' weights) + 4 C D (the aggregate) + 4 N (p)."""
+    import torch
+    from fedamw_amd import _lib
+    N = len(fed.mine)
+    nbytes = 4.0 * N * wl['C'] * wl['D'] + 4.0 * wl['C'] * wl['D'] + 4.0 * N
+    t = max(fed.t - 1, 0)
+    if fed.mixture is not None:
+        p = fed.p_slice(fed.mixture.p) if fed.zshard else fed.mixture.p
+        fn = lambda: fed.agg.run(fed.trainer.W_out, p, fed.W_g)     # noqa: E731
+    else:
+        fn = lambda: fed.plan.round(t, fed.lr, _lib.PHASE_AGGREGATE)  # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    ev = []
+    for _ in range(reps):
+        a, b = _lib.Timer(), _lib.Timer()
+        a.record()
+        fn()
+        b.record()
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {'kernel': 'fs_aggregate', 'ms': ms, 'alg_bytes': nbytes, 'achieved': gbs, 'unit': 'GB/s',
+            'peak': HBM_PEAK_GBS, 'frac': gbs / HBM_PEAK_GBS, 'clients': N, 'launches': reps,
+            'note': 'HIP events, %d launches back to back after the timed rounds, the round\'s own inputs' % reps}
 
 
 def _solver_name():
@@ -761,6 +853,7 @@ def worker(args):
         'config': dict(workload=main['workload'], **main['config']),
         'dist': dinfo,
         'roofline': main['roofline'],
+        'aggregate': main['aggregate'],
         'final_test_acc': main['final_test_acc'],
         'device_settle_ms': main['device_settle_ms'],
         'device_settle_kind': main['device_settle_kind'],
@@ -776,7 +869,7 @@ def worker(args):
             r = run_workload(lw, ws, rank, dev, k, w, 100, cpu_s)
             obj = {'workload': r['workload'], 'value': r['value'], 'unit': 'client-rounds/s',
                    'ms_per_round': r['ms_per_step'], 'rounds_timed': k, 'warmup': w, 'scaling': r['scaling'],
-                   'roofline': r['roofline'], 'final_test_acc': r['final_test_acc'],
+                   'roofline': r['roofline'], 'aggregate': r['aggregate'], 'final_test_acc': r['final_test_acc'],
                    'device_settle_ms': r['device_settle_ms'], 'device_settle_kind': r['device_settle_kind'],
                    'leg_wall_s': time.perf_counter() - t0}
             for key in ('fedamw', 'cpu_baseline'):

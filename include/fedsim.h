@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 14
+#define FS_ABI_VERSION 15
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -103,6 +103,11 @@ const char* fs_last_error(void);
  *                      none), -1 = none, n > 0 = n; bitwise the same results
  *   split_pipe         (ABI 14) fs_local_train_plan's choice of the pipe form (FS_G_PIPE):
  *                      0 = by shape, 1 = wherever it fits (G = ld / 1024), -1 = never
+ *   split_dbuf         (ABI 15) split form on full slices (8 waves x 2 tiles, or the narrow
+ *                      chained 4 x 1) with 16 < B <= 32: the double-buffered instance
+ *                      (local_train_dbuf.hip: the rows streamed ahead of the hand-off);
+ *                      1 = wherever it covers; 0 = by shape (not chosen: measured a tie at
+ *                      configs 2 and 5, slower at config 1); -1 = never; bitwise the same results
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -131,6 +136,7 @@ typedef struct fs_tuning {
   int mix_poll_delay;
   int split_poll_delay;
   int split_pipe;
+  int split_dbuf;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -333,6 +339,17 @@ int fs_mix_solve_last_mode(void);
  * fs_mix_solve_blocked launch when it ran the qmc solver -- its workgroups K and clients per
  * lane (4 or 8; K = ceil(ldN / (16 * lane_clients))) -- else 0 and 0. */
 int fs_mix_solve_last_layout(int* workgroups, int* lane_clients);
+/* (ABI 15) Diagnostic (host state only): the kernel the calling thread's last fs_local_train
+ * launched -- FS_LT_SINGLE (1, one workgroup per client), FS_LT_SPLIT (2), FS_LT_DBUF (3, the
+ * split form's double-buffered instance: the rows streamed ahead of the hand-off),
+ * FS_LT_PAIR (4), FS_LT_PIPE (5), FS_LT_TEAMS (6); 0 = none yet. */
+#define FS_LT_SINGLE 1
+#define FS_LT_SPLIT 2
+#define FS_LT_DBUF 3
+#define FS_LT_PAIR 4
+#define FS_LT_PIPE 5
+#define FS_LT_TEAMS 6
+int fs_local_train_last_kernel(void);
 
 /* ------------------------------------------------------------------------- *
  * Random Fourier feature map.  Replaces RFF's use in feature_mapping
@@ -379,8 +396,9 @@ int fs_hetero(const float* d_phi, int64_t ld, const int64_t* d_row_off, int N, i
  *                       call after it: the fused evaluation's finaliser rides on the
  *                       next AGGREGATE launch, and any call that trains or does not
  *                       aggregate runs a pending one first -- make one more
- *                       fs_plan_round call (phases 0 will do) before reading
- *                       d_eval_hist after a TRAIN-only call.  The pending evaluation reads d_W_g
+ *                       fs_plan_round call (phases 0 will do) or, since ABI 15,
+ *                       fs_plan_eval_flush before reading d_eval_hist after a
+ *                       TRAIN-only call.  The pending evaluation reads d_W_g
  *                       as it is when that next call's launches run: the caller
  *                       must NOT write d_W_g (its own aggregate, an all-reduce into
  *                       it, a copy) between the deferring call and the next
@@ -450,6 +468,11 @@ int fs_plan_create(const fs_plan_desc* desc, fs_plan** out);
 int fs_plan_destroy(fs_plan* plan);
 int fs_plan_shuffle(fs_plan* plan, const int64_t* h_seeds, int t);
 int fs_plan_round(fs_plan* plan, int t, float lr, int phases, const float* d_p_override, void* stream);
+/* ABI 15: complete on `stream` every evaluation the plan still holds (a deferred one not yet
+ * carried by a TRAIN launch, a fused one whose finaliser waits for the next AGGREGATE), so
+ * d_eval_hist is final once the stream reaches this point.  Replaces the "one more
+ * fs_plan_round call with phases 0" of ABI 14 (which still works). */
+int fs_plan_eval_flush(fs_plan* plan, void* stream);
 /* ABI 7 (device replay only; call before the first fs_plan_shuffle): generate the shuffles of
  * `rounds` consecutive rounds (a chunk: rounds cK .. cK+K-1) with ONE fs_randperm_device launch
  * into one of two chunk slots.  fs_plan_shuffle then only collects round t's seeds and launches

@@ -77,6 +77,8 @@ int local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const 
 
 // split-client launcher (local_train_split.hip): G workgroups per client
 int launch_local_train_split(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
+// the kernel the calling thread's last fs_local_train launched (FS_LT_*, fs_local_train_last_kernel)
+void set_last_lt_kernel(int k);
 // pair-client launcher (local_train_pair.hip): G workgroups per group, two clients per group
 int launch_local_train_pair(const LTParams& P, int G, void* ws, int64_t ws_bytes, hipStream_t st);
 // pipelined split launcher (local_train_pipe.hip): G workgroups per client, hand-off by row tile

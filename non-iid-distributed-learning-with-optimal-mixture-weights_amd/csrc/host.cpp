@@ -61,6 +61,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": split_poll_delay must be in [-1, 4096]");
   if (t && (t->split_pipe < -1 || t->split_pipe > 1))
     return fail(FS_EINVAL, std::string(fn) + ": split_pipe must be -1, 0 or 1");
+  if (t && (t->split_dbuf < -1 || t->split_dbuf > 1))
+    return fail(FS_EINVAL, std::string(fn) + ": split_dbuf must be -1, 0 or 1");
   return FS_OK;
 }
 

@@ -392,6 +392,10 @@ static int launch_lt(const LTParams& P, int grid, hipStream_t st) {
 
 using namespace fs;
 
+static thread_local int t_last_lt = 0;
+void fs::set_last_lt_kernel(int k) { t_last_lt = k; }
+extern "C" int fs_local_train_last_kernel(void) { return t_last_lt; }
+
 extern "C" int fs_local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, const int32_t* d_labels,
                               const int32_t* d_perms, const int32_t* d_order, int N, int C, int B, int E,
                               float lr, float mu, int prox, float lam, int reg, int chained,
@@ -422,6 +426,7 @@ int fs::local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, co
     P.fuse_part = fuse->part;
   }
   if (G > 1) {
+    set_last_lt_kernel((G & FS_G_PIPE) ? FS_LT_PIPE : (G & FS_G_PAIR) ? FS_LT_PAIR : (G & FS_G_TEAMS) ? FS_LT_TEAMS : FS_LT_SPLIT);
     const int rc = (G & FS_G_PIPE)   ? launch_local_train_pipe(P, G & (FS_G_PAIR - 1), d_ws, ws_bytes, st)
                    : (G & FS_G_PAIR) ? launch_local_train_pair(P, G & (FS_G_PAIR - 1), d_ws, ws_bytes, st)
                                      : launch_local_train_split(P, G, d_ws, ws_bytes, st);
@@ -429,6 +434,7 @@ int fs::local_train(const float* d_phi, int64_t ld, const int64_t* d_row_off, co
     FS_LAUNCH_CHECK();
     return FS_OK;
   }
+  set_last_lt_kernel(FS_LT_SINGLE);
   const int grid = chained ? 1 : N;
   const int RT = B <= 16 ? 1 : (B <= 32 ? 2 : 4);
   const int CT = C <= 16 ? 1 : 2;

@@ -553,12 +553,13 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
     // ---- the g values of a row tile, once its four columns are flagged ----
     float gB[8];
     auto take_g = [&](int rt) {
-      unsigned sp = 0;
+      // (64-bit: 64 x a fs_tuning.spin_limit of 2^26 or more would wrap in 32 bits)
+      unsigned long long sp = 0;
       for (;;) {
         typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
         const uintx4 f = *reinterpret_cast<volatile const uintx4*>(&gfl[par][rt][0]);
         if ((f[0] == tag32) & (f[1] == tag32) & (f[2] == tag32) & (f[3] == tag32)) break;
-        if (dead || ++sp > 64u * X.spin_limit) {
+        if (dead || ++sp > 64ull * X.spin_limit) {
           if (lane == 0) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           dead = true;
           break;

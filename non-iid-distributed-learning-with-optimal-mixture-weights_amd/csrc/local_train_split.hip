@@ -58,6 +58,9 @@ constexpr int SP_ERR_BYTES = 256;         // error block at the END of the works
 #define SP_E3 0
 #endif
 constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
+#ifndef SP_NARROW_MIDFETCH
+#define SP_NARROW_MIDFETCH 0
+#endif
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -524,6 +527,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         }
         SP_STAMP(4)
       }
+      // (narrow chained instances, SP_NARROW_MIDFETCH) the next step's labels and row indices go out
+      // here, after the polls returned and ahead of the row stream: the step's end then waits for
+      // them alone instead of for every row load issued before them (in-order vmcnt)
+      constexpr bool MID_FETCH = !TOP_FETCH && SP_NARROW_MIDFETCH;
+      if constexpr (MID_FETCH) fetch_next();
       // the first SP_EARLY of this wave's next-step row loads go out here, behind the hand-off's
       // polls (which have all returned): they stream through S2, the softmax and S3 instead of
       // waiting for the backward (FedAvg / FedAMW on full slices; the prox anchor's loads would
@@ -701,7 +709,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       } else {
         bwd(std::false_type{}, std::false_type{}, E0{});
       }
-      if constexpr (!TOP_FETCH) fetch_next();
+      if constexpr (!TOP_FETCH && !MID_FETCH) fetch_next();
       if (ilv) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -882,8 +890,22 @@ static void launch_split_teams(const LTParams& P, const SplitWS& X, int grid, si
   else launch_split_s<RT, G, false, 0, 2>(P, X, grid, lds, st);
 }
 
+// the double-buffered instance (local_train_dbuf.hip, round 6): where it covers the launch and
+// fs_tuning.split_dbuf asks for it (1 = wherever it covers; 0 = by shape: not chosen -- measured a
+// tie at configs 2 and 5 and slower at config 1; -1 = never); bitwise the same
+bool dbuf_covers(int C, int B, int64_t ld, int G, int chained, int prox, int* waves_out);
+int launch_local_train_dbuf(const LTParams& P, int G, const SplitWS& X, int grid, size_t lds, hipStream_t st);
+static bool dbuf_by_shape(const LTParams& P, int G) {
+  if (tuning().split_dbuf <= 0 || tuning().split_early < 0) return false;
+  return dbuf_covers(P.C, P.B, P.ld, G, P.chained, P.prox, nullptr);
+}
+
 template <int RT, int G>
 static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if (RT == 2 && dbuf_by_shape(P, G) && launch_local_train_dbuf(P, G, X, grid, lds, st) == FS_OK) {
+    set_last_lt_kernel(FS_LT_DBUF);
+    return;
+  }
   // early row issue where every workgroup's slice is full (NT = G * 16 tiles)
   // (fs_tuning.split_early: 0 = by shape, -1 = never)
   // Depth per width (profiles/r03/split_early_ab2.txt, launch ms): at G = 2 (128 KB of rows per
@@ -1024,7 +1046,9 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   // rows on 128 groups of 2: 395-409 vs 419-448 us per launch for the pair form (G = 4) and
   // 285-302 vs 300-310 us at config 2's 100 clients, where the split form stays
   // (profiles/r05/pipe_vs_forms.txt); config 5's G = 16: 6.5 vs 4.9 ms, not chosen)
-  if (!(want > 1 && want < FS_G_PAIR) && NT % 16 == 0 && tuning().split_pipe >= 0) {
+  // (entered for an automatic choice or a pipe request only: an explicit split, pair or team
+  // request is answered by its own form, never by the pipe form under split_pipe = 1)
+  if ((want == 0 || (want & FS_G_PIPE)) && NT % 16 == 0 && tuning().split_pipe >= 0) {
     const int g = NT / 16;
     const bool by_shape = tuning().split_pipe == 0 && want == 0 && tuning().train_form == 0 && !chained &&
                           !prox && g <= 4 && N > pipe_groups(N, g, 0, cus);

@@ -521,6 +521,22 @@ static int flush_eval(fs_plan* p, hipStream_t st) {
   return fs_eval(d.d_phi_t, d.ld, d.d_labels_t, d.n_t, d.d_W_g, d.C, d.d_eval_hist + 2 * (int64_t)te, d.d_eval_ws, st);
 }
 
+// ABI 15: complete every evaluation this plan still holds -- a deferred one
+// not yet carried by a TRAIN launch (as its own fs_eval launch) and a fused one whose finaliser
+// waits for the next AGGREGATE -- so d_eval_hist is final once `stream` reaches this point.
+extern "C" int fs_plan_eval_flush(fs_plan* p, void* stream) {
+  FS_REQUIRE(p, "bad arguments");
+  const fs_plan_desc& d = p->d;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (p->fin_pending >= 0) {
+    const fs::EvalFinalize f{d.d_eval_ws, p->fuse_E, (int)d.n_t, d.d_eval_hist + 2 * (int64_t)p->fin_pending};
+    p->fin_pending = -1;
+    const int rc = fs::eval_finalize_launch(f.part, f.nb, f.n, f.out, st);
+    if (rc != FS_OK) return rc;
+  }
+  return flush_eval(p, st);
+}
+
 extern "C" int fs_plan_round(fs_plan* p, int t, float lr, int phases, const float* d_p_override, void* stream) {
   FS_REQUIRE(p && t >= 0, "bad arguments");
   const fs_plan_desc& d = p->d;

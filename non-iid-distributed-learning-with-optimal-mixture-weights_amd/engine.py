@@ -294,6 +294,11 @@ class RoundPlan:
         assert seeds.shape == (self.npasses,)
         _lib.check(_lib.lib().fs_plan_shuffle(self._h, seeds.ctypes.data, int(t)), 'fs_plan_shuffle')
 
+    def eval_flush(self):
+        """fs_plan_eval_flush (ABI 15): complete any evaluation still deferred, so the eval
+        history is final on the current stream."""
+        _lib.check(_lib.lib().fs_plan_eval_flush(self._h, _lib.stream_ptr()), 'fs_plan_eval_flush')
+
     def round(self, t, lr, phases, p_override=None):
         _lib.check(_lib.lib().fs_plan_round(self._h, int(t), float(lr), int(phases),
                                             None if p_override is None else _lib.ptr(p_override),

@@ -333,8 +333,8 @@ class Federation:
     def results(self):
         """Single host sync: (train_loss, test_loss, test_acc) CPU float32 tensors."""
         R, D = self.t, self.D
-        if 0 < R < self.R and self.defer_eval:
-            self.plan.round(R - 1, self.lr, 0)           # runs a deferred evaluation, if any
+        if 0 < R and self.defer_eval:
+            self.plan.eval_flush()                       # completes a deferred evaluation, if any (ABI 15)
         self.trainer.check_errors()
         if self.mixture is not None:
             self.mixture.check_errors()

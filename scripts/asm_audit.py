@@ -19,7 +19,8 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, 'non-iid-distributed-learning-with-optimal-mixture-weights_amd', 'csrc')
 KERNELS = {'pair': ('local_train_pair.hip', r'^_Z\w*local_train_pair_kernel\w*:'),
-           'pipe': ('local_train_pipe.hip', r'^_Z\w*local_train_pipe_kernel\w*:')}
+           'pipe': ('local_train_pipe.hip', r'^_Z\w*local_train_pipe_kernel\w*:'),
+           'dbuf': ('local_train_dbuf.hip', r'^_Z\w*local_train_dbuf_kernel\w*:')}
 REG = re.compile(r'\bv\[(\d+):(\d+)\]|\bv(\d+)\b')
 
 

@@ -33,8 +33,11 @@ def main():
     ap.add_argument('--teams', action='store_true', help='the team form at width --G (team 0 stamped)')
     ap.add_argument('--pipe', action='store_true', help='the pipe form at width --G')
     ap.add_argument('--prox', action='store_true', help="FedProx's prox term (mu = 1e-3), ridge off")
+    ap.add_argument('--dbuf', choices=['auto', 'on', 'off'], default='auto',
+                    help="fs_tuning.split_dbuf: the split form's double-buffered instance (round 6)")
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
+    fedamw_amd._lib.set_tuning(split_dbuf={'auto': 0, 'on': 1, 'off': -1}[a.dbuf])
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
     dev = torch.device('cuda')

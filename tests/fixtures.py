@@ -91,5 +91,15 @@ def horizon_rtol(name, what='W'):
     return rec['rtol_' + what]
 
 
+def horizon_rtol_rounds(name, what='W'):
+    """Per-round bounds of a horizon case (round 6): round t is held to
+    max(1e-5, 2 max_{s <= t} delta(s)) -- the fp32-vs-fp64 drift the restatement accumulates by
+    round t -- instead of the whole run's worst round.  ``what`` in 'W', 'loss' (p is checked
+    after the last round only: ``horizon_rtol(name, 'p')``)."""
+    rec = HORIZON_DRIFT[name]
+    d = np.maximum.accumulate(np.asarray(rec['delta_%s_per_round' % what], np.float64))
+    return np.maximum(1e-5, 2.0 * d)
+
+
 def acc_tol(d):
     return 100.0 / len(d['y_test']) + 1e-4

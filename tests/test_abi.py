@@ -44,6 +44,7 @@ def test_abi_version():
     (lambda L: L.fs_plan_set_shuffle_chunk(None, 8), 'bad arguments'),
     (lambda L: L.fs_plan_shuffle_flush(None), 'bad arguments'),
     (lambda L: L.fs_plan_eval_blocks(None), 'bad arguments'),
+    (lambda L: L.fs_plan_eval_flush(None, None), 'bad arguments'),
     (lambda L: L.fs_timer_create(None), 'null'),
     (lambda L: L.fs_timer_record(None, None), 'null'),
     (lambda L: L.fs_timer_elapsed_ms(None, None, None), 'null'),

@@ -63,9 +63,9 @@ def test_spawn_launch_timeout(tmp_path, capfd):
 
 
 def test_spawn_teardown_timeout(tmp_path, capfd):
-    """The default bound counts only from the first worker that exits 0: a rank still running
-    that long after rank 0 finished is stopped (124); a long but healthy run with no finished
-    rank is not cut (no whole-run bound by default)."""
+    """The teardown bound counts from the first worker that exits 0 (or rank 0's result line): a
+    rank still running that long after rank 0 finished is stopped (124); a run whose ranks all
+    finish inside it is not cut."""
     w = tmp_path / 'w.py'
     w.write_text('import os, sys, time\nif os.environ["RANK"] == "0":\n    print("{}", flush=True)\n    sys.exit(0)\n'
                  'time.sleep(600)\n')
@@ -77,7 +77,24 @@ def test_spawn_teardown_timeout(tmp_path, capfd):
     slow = tmp_path / 'slow.py'
     slow.write_text('import time\ntime.sleep(4)\nprint("{}", flush=True)\n')
     assert bench.spawn(2, [sys.executable, str(slow)], teardown=2.0) == 0
-    assert bench.parse([]).launch_timeout == 0.0
+    # the default whole-run bound is finite and scaled to the rounds asked for
+    a = bench.parse([])
+    assert a.launch_timeout == bench.default_launch_timeout(a) >= 1800.0
+    assert bench.parse(['--steps', '1000']).launch_timeout > a.launch_timeout
+    assert bench.parse(['--launch-timeout', '0']).launch_timeout == 0.0
+
+
+def test_spawn_teardown_counts_from_the_result_line(tmp_path, capfd):
+    """Every rank hangs after rank 0 printed its result line (none exits): the teardown bound
+    counts from that line, so the launch still ends (124) with the line relayed."""
+    w = tmp_path / 'w.py'
+    w.write_text('import os, time\nif os.environ["RANK"] == "0":\n    print("{\\"metric\\": 1}", flush=True)\n'
+                 'time.sleep(600)\n')
+    import time
+    t0 = time.time()
+    assert bench.spawn(2, [sys.executable, str(w)], teardown=2.0) == 124
+    assert time.time() - t0 < 60
+    assert '{"metric": 1}' in capfd.readouterr().out
 
 
 def test_gpus_must_match_world_size(monkeypatch):

@@ -128,6 +128,11 @@ def test_pipe_planner(amd):
     with amd.lib.tuning(split_pipe=1):
         g, ws = plan(100, 10, 32, 2048)
         assert g == 2 | P and ws > 256
+        # explicit split / pair / team requests keep their own form under split_pipe = 1
+        # (they used to come back as the pipe form)
+        assert plan(100, 10, 32, 2048, want=4)[0] == 4
+        assert plan(100, 10, 32, 2048, want=4 | amd.lib.G_PAIR)[0] == 4 | amd.lib.G_PAIR
+        assert plan(100, 10, 32, 2048, want=4 | amd.lib.G_TEAMS)[0] == 4 | amd.lib.G_TEAMS
     with amd.lib.tuning(split_pipe=-1):
         assert not plan(100, 10, 32, 2048)[0] & P
 
