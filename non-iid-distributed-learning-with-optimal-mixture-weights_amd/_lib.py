@@ -252,7 +252,7 @@ def stream_ptr(stream=None):
 # the device sources each measured kernel is compiled from (its own file + the headers it includes)
 KERNEL_SOURCES = {
     'local_train': ('local_train.hip', 'local_train_split.hip', 'local_train_pair.hip', 'local_train_pipe.hip',
-                    'split_common.h', 'common.h',
+                    'local_train_dbuf.hip', 'split_common.h', 'common.h',
                     'eval_rows.h', 'lanes.h'),
     'mix_solve': ('mixture.hip', 'common.h', 'lanes.h'),
     'mix_z': ('mix_z.hip', 'common.h'),

@@ -58,9 +58,6 @@ constexpr int SP_ERR_BYTES = 256;         // error block at the END of the works
 #define SP_E3 0
 #endif
 constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
-#ifndef SP_NARROW_MIDFETCH
-#define SP_NARROW_MIDFETCH 0
-#endif
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -475,6 +472,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         // 0..G-1 with the own partial at position g: identical bits in every partner
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += HC) {
+          // (measured and dropped, round 6: waves holding no exchanged value at slot m skipping
+          // their dummy polls -- config 5 4.76 -> 4.99 ms per launch, config 2 285 -> 288 us;
+          // profiles/r06/poll_skip_ab.txt.  The dummy round trips act as the first-poll sleep does.)
           auto poll = [&]() {
 #pragma unroll
             for (int m = 0; m < M; ++m) {
@@ -527,11 +527,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         }
         SP_STAMP(4)
       }
-      // (narrow chained instances, SP_NARROW_MIDFETCH) the next step's labels and row indices go out
-      // here, after the polls returned and ahead of the row stream: the step's end then waits for
-      // them alone instead of for every row load issued before them (in-order vmcnt)
-      constexpr bool MID_FETCH = !TOP_FETCH && SP_NARROW_MIDFETCH;
-      if constexpr (MID_FETCH) fetch_next();
       // the first SP_EARLY of this wave's next-step row loads go out here, behind the hand-off's
       // polls (which have all returned): they stream through S2, the softmax and S3 instead of
       // waiting for the backward (FedAvg / FedAMW on full slices; the prox anchor's loads would
@@ -709,7 +704,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       } else {
         bwd(std::false_type{}, std::false_type{}, E0{});
       }
-      if constexpr (!TOP_FETCH && !MID_FETCH) fetch_next();
+      if constexpr (!TOP_FETCH) fetch_next();
       if (ilv) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
