@@ -108,3 +108,27 @@ def test_defaults_are_config2():
     a = bench.parse([])
     assert (a.config, a.algo, a.clients, a.D, a.C, a.custom) == (2, 'fedavg', 100, 2048, 10, False)
     assert [c for c, _, _ in bench.LEGS] == [4, 3, 5]
+
+
+def test_cpu_fedamw_round_is_one_whole_oracle_round():
+    """bench.cpu_fedamw_round (config 5's measured CPU baseline, round 6): one whole FedAMW round of
+    the oracle -- every client's training, the Z GEMM on every validation row, all R x ceil(n_v / 16)
+    p-SGD steps -- on a tiny workload; the sample text states what was timed, and the global torch
+    generator is left where it was (the bench's RNG use must not move the workload's)."""
+    import numpy as np
+    import torch
+    rs = np.random.RandomState(3)
+    N, n, D, C, nv = 4, 40, 64, 3, 37
+    d = {'X_train': [torch.from_numpy(rs.rand(n, D).astype(np.float32)) for _ in range(N)],
+         'y_train': [torch.from_numpy(rs.randint(0, C, n)) for _ in range(N)],
+         'X_val': torch.from_numpy(rs.rand(nv, D).astype(np.float32)), 'y_val': torch.from_numpy(rs.randint(0, C, nv)),
+         'X_test': torch.from_numpy(rs.rand(50, D).astype(np.float32)), 'y_test': torch.from_numpy(rs.randint(0, C, 50))}
+    torch.manual_seed(7)
+    before = torch.get_rng_state()
+    out = bench.cpu_baseline(d, {'D': D, 'C': C, 'algo': 'fedamw'}, 1.0, True, 5, None, whole_max_s=60.0)
+    assert out['measured'] is True and out['extrapolation_factor'] == 1.0 and out['value'] > 0
+    assert ('%d client trainings' % N) in out['sample'] and ('all %d p-SGD steps' % (5 * ((nv + 15) // 16))) in out['sample']
+    assert torch.equal(torch.get_rng_state(), before)
+    # without the whole-round budget the FedAMW sample stays an extrapolation, labelled as one
+    out = bench.cpu_baseline(d, {'D': D, 'C': C, 'algo': 'fedamw'}, 1.0, True, 5, None)
+    assert out['measured'] is False and 'extrapolated' in out['sample']
