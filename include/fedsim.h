@@ -40,7 +40,7 @@ extern "C" {
 #define FS_EHIP (-2)
 #define FS_EUNSUPPORTED (-3)
 
-#define FS_ABI_VERSION 15
+#define FS_ABI_VERSION 16
 
 /* ABI version and the last error message of the calling thread. */
 int fs_abi_version(void);
@@ -108,6 +108,11 @@ const char* fs_last_error(void);
  *                      (local_train_dbuf.hip: the rows streamed ahead of the hand-off);
  *                      1 = wherever it covers; 0 = by shape (not chosen: measured a tie at
  *                      configs 2 and 5, slower at config 1); -1 = never; bitwise the same results
+ *   split_mb           (ABI 16) split form with 16 < B <= 32: the classes on the 16-block
+ *                      v_mfma_f32_4x4x1_16b_f32 in ceil(C / 4) blocks of 4 (the "mb" instances,
+ *                      local_train_split.hip) instead of v_mfma_f32_16x16x4_f32 padded to 16;
+ *                      0 = by shape, 1 = wherever it fits, -1 = never.  Same steps and hand-off,
+ *                      the products summed in another order (within the oracle's fp32 tolerance)
  * ------------------------------------------------------------------------- */
 #define FS_SOLVER_AUTO 0
 #define FS_SOLVER_REG 1
@@ -137,6 +142,7 @@ typedef struct fs_tuning {
   int split_poll_delay;
   int split_pipe;
   int split_dbuf;
+  int split_mb;
 } fs_tuning;
 
 int64_t fs_tuning_size(void);
@@ -342,13 +348,15 @@ int fs_mix_solve_last_layout(int* workgroups, int* lane_clients);
 /* (ABI 15) Diagnostic (host state only): the kernel the calling thread's last fs_local_train
  * launched -- FS_LT_SINGLE (1, one workgroup per client), FS_LT_SPLIT (2), FS_LT_DBUF (3, the
  * split form's double-buffered instance: the rows streamed ahead of the hand-off),
- * FS_LT_PAIR (4), FS_LT_PIPE (5), FS_LT_TEAMS (6); 0 = none yet. */
+ * FS_LT_PAIR (4), FS_LT_PIPE (5), FS_LT_TEAMS (6), FS_LT_MB (7, ABI 16: the split form's
+ * 4x4x1 multi-block instances, fs_tuning.split_mb); 0 = none yet. */
 #define FS_LT_SINGLE 1
 #define FS_LT_SPLIT 2
 #define FS_LT_DBUF 3
 #define FS_LT_PAIR 4
 #define FS_LT_PIPE 5
 #define FS_LT_TEAMS 6
+#define FS_LT_MB 7
 int fs_local_train_last_kernel(void);
 
 /* ------------------------------------------------------------------------- *

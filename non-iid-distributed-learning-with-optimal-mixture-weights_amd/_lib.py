@@ -72,12 +72,12 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 PHASE_TRAIN, PHASE_AGGREGATE, PHASE_EVAL, PHASE_EVAL_DEFER = 1, 2, 4, 8
 G_PAIR = 256             # fs_local_train_plan: G | G_PAIR = the pair-client form at width G (ABI 10)
 G_TEAMS = 512            # fs_local_train_plan: G | G_TEAMS = the team form at width G (ABI 13)
-LT_KERNELS = {1: 'single', 2: 'split', 3: 'dbuf', 4: 'pair', 5: 'pipe', 6: 'teams'}   # fs_local_train_last_kernel (ABI 15)
+LT_KERNELS = {1: 'single', 2: 'split', 3: 'dbuf', 4: 'pair', 5: 'pipe', 6: 'teams', 7: 'mb'}   # fs_local_train_last_kernel (ABI 15; mb: 16)
 G_PIPE = 1024            # fs_local_train_plan: G | G_PIPE = the pipelined split form at width G (ABI 14)
 ERR_BLOCK = 256          # the error block at the end of every exchange workspace (include/fedsim.h)
 SOLVER_NAMES = {0: 'none', 1: 'reg', 2: 'mc', 3: 'staged', 4: 'global', 5: 'reg2', 6: 'wave', 8: 'quad', 9: 'qmc', 10: 'bin'}
@@ -92,7 +92,8 @@ class Tuning(C.Structure):
                 ('split_early', C.c_int), ('mix_qmc_lane_clients', C.c_int),
                 ('mix_quad_loaders', C.c_int), ('split_teams', C.c_int),
                 ('mix_poll_delay', C.c_int), ('split_poll_delay', C.c_int), ('split_pipe', C.c_int),
-                ('split_dbuf', C.c_int)]
+                ('split_dbuf', C.c_int),
+                ('split_mb', C.c_int)]
 
 
 class PlanDesc(C.Structure):

@@ -63,6 +63,8 @@ static int check_tuning(const fs_tuning* t, const char* fn) {
     return fail(FS_EINVAL, std::string(fn) + ": split_pipe must be -1, 0 or 1");
   if (t && (t->split_dbuf < -1 || t->split_dbuf > 1))
     return fail(FS_EINVAL, std::string(fn) + ": split_dbuf must be -1, 0 or 1");
+  if (t && (t->split_mb < -1 || t->split_mb > 1))
+    return fail(FS_EINVAL, std::string(fn) + ": split_mb must be -1, 0 or 1");
   return FS_OK;
 }
 

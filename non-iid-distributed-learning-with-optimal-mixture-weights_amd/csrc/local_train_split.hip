@@ -58,6 +58,16 @@ constexpr int SP_ERR_BYTES = 256;         // error block at the END of the works
 #define SP_E3 0
 #endif
 constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
+// mb instances: the backward's image and g words read one row block ahead (SP_MB_BWD_PF; without
+// it the reads waited just in time: config 2 313 -> 288 us per launch, config 5 5.99 -> 5.58 ms,
+// profiles/r06/mb_ab.txt), and the next step's tile-0 forward at the step's end (SP_MB_PRE, where
+// it fits: PRE_OK in the kernel)
+#ifndef SP_MB_BWD_PF
+#define SP_MB_BWD_PF 1
+#endif
+#ifndef SP_MB_PRE
+#define SP_MB_PRE 1
+#endif
 
 // Diagnostic build only (-DFS_STAMPS): per-phase cycle sums of wave 0 of every workgroup,
 // written to a side buffer that nothing else reads (never in the shipped library).
@@ -74,6 +84,54 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 #else
 #define SP_STAMP(k)
 #endif
+
+// ---- the mb instances' MFMA pieces (v_mfma_f32_4x4x1_16b_f32; layouts at the kernel) ----
+template <int CBSZ, int ABID, int BLGP>
+__device__ __forceinline__ floatx4 mfma4x4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, CBSZ, ABID, BLGP);
+}
+// forward of one 16-column group q of a tile: 4 components x RT row tiles x CB class blocks
+template <int Q, int RT, int CB>
+__device__ __forceinline__ void mb_fwd_q(floatx4 (&acc)[RT][CB], const float4 (&xt)[RT][4], const float4 (&wt)[CB]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) acc[rt][cb] = mfma4x4<2, Q, 0>(comp(wt[cb], e), comp(xt[rt][Q], e), acc[rt][cb]);
+}
+// backward of one batch row: the CB class blocks' gradients of one tile
+template <int CB>
+__device__ __forceinline__ void mb_bwd_row(floatx4 (&ga)[CB], float a, float g) {
+  ga[0] = mfma4x4<0, 0, 4>(a, g, ga[0]);
+  if constexpr (CB > 1) ga[1] = mfma4x4<0, 0, 5>(a, g, ga[1]);
+  if constexpr (CB > 2) ga[2] = mfma4x4<0, 0, 6>(a, g, ga[2]);
+  if constexpr (CB > 3) ga[3] = mfma4x4<0, 0, 7>(a, g, ga[3]);
+}
+__device__ __forceinline__ void mb_swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void mb_swap16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+// the four k-group partials of a forward accumulator summed: lane 16 lg + l16 of the result holds
+// register mb_perm(lg) of acc (row l16) summed over lg = 0..3, as (k0 + k2) + (k1 + k3)
+__device__ __forceinline__ float mb_kgroup_sum(floatx4 a) {
+  float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3];
+  mb_swap32(r0, r1);
+  mb_swap32(r2, r3);
+  float s01 = r0 + r1, s23 = r2 + r3;
+  mb_swap16(s01, s23);
+  return s01 + s23;
+}
+__device__ __forceinline__ int mb_perm(int lg) { return ((lg & 1) << 1) | (lg >> 1); }
+// offset of (row, class) in a wave's mb partial-logit block [rt][class block][j][l16]
+template <int CB>
+__device__ __forceinline__ int zp_off_mb(int r, int c) { return ((r >> 4) * CB + (c >> 2)) * 64 + (c & 3) * 16 + (r & 15); }
 
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
@@ -102,10 +160,31 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 // at 4 tiles per slice left waves 4-7 without a tile and guarded tile 1 of every wave: the
 // compiler then waited vmcnt(0) for the whole next-step row stream at that guard's join, inside
 // the backward -- 5.4 k of config 1's 12.1 k cycles per step, profiles/r05b/stamps_c1.txt.)
-template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
+// MBK (round 6, the "mb" instances): 0 = the classes on v_mfma_f32_16x16x4_f32 (padded to 16);
+// 1..4 = on v_mfma_f32_4x4x1_16b_f32 in MBK blocks of 4 classes (C = 10 pads to 12, C = 2 to 4).
+// The 16-block instruction runs at the f32 MFMA rate, 8 cycles per SIMD with the kernel's operand
+// pattern (scripts/probe/mb_fwd_rate.hip, profiles/r06/mb_fwd_rate_probe.txt: one wave's forward
+// 1,576 vs 2,048 cycles at C = 10; a probe reusing one register pair issued faster and misled),
+// so per step the MFMA cycles scale with ceil(C / 4) / 4: 3/4 at C = 10, 1/2 at C <= 8, 1/4 at C <= 4.
+// Operand layouts (checked on one wave against a CPU product, scripts/probe/mb_layout.hip):
+//   rows      xf[i][rt][q] as in the 16x16x4 form: lane (l16, lg), component e = X[16 rt + l16][16 q + 4 lg + e]
+//   weights   wr[i][cb], lane 16 lg + 4 q + j, component e = W[4 cb + j][16 q + 4 lg + e] (the tile's columns)
+//   forward   acc[rt][cb] += mfma(A = wr[i][cb].e broadcast from block q of each 16-lane group
+//             (cbsz 2, abid q), B = xf[i][rt][q].e): lane 16 lg + l16, register j = the partial
+//             logit (row 16 rt + l16, class 4 cb + j) over k-group lg; the four k-groups are summed
+//             with v_permlane32_swap / v_permlane16_swap (mb_kgroup_sum)
+//   backward  ga[i][cb] += mfma(A = image row r, lane 16 lg + 4 q + e at column 16 q + 4 lg + e,
+//             B = g row r, lane 16 s + 4 x + j = g[r][4 s + j], broadcast from 16-lane group cb (blgp 4 + cb)):
+//             lane 16 lg + 4 q + j, register e = grad[4 cb + j][16 q + 4 lg + e] -- wr's own layout
+// Same steps, hand-off, softmax and schedule as the 16x16x4 instances; the products are summed in
+// another order (within the fp32 tolerance of the oracle, not bitwise the other forms).
+template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW, int MBK = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTParams P, SplitWS X) {
   static_assert(TEAMS == 1 || TEAMS == 2, "teams");
   static_assert(WAVES == SP_WAVES || (WAVES == 4 && TEAMS == 1), "waves");
+  static_assert(MBK >= 0 && MBK <= 4 && (MBK == 0 || TEAMS == 1), "mb");
+  constexpr bool MB = MBK > 0;
+  constexpr int NQ = MB ? MBK : 4;                 // weight registers per tile: q (16x16x4) or class block (mb)
   constexpr int NW = WAVES / TEAMS;                // waves per client lane
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
@@ -134,6 +213,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   const int team = TEAMS > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / NTH) : 0;
   const int tid = (int)threadIdx.x - team * NTH, lane = tid & 63, l16 = lane & 15, lg = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform for the compiler
+  const int mq = (lane >> 2) & 3, mi = lane & 3;            // mb weight lanes: 16 lg + 4 mq + mi
   auto& zpart = zpart_t[team];
   auto& gbuf = gbuf_t[team];
   auto& zsum = zsum_t[team];
@@ -211,7 +291,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---- weights (and prox anchor) of this slice into registers: the round-start model ----
-  float4 wr[TPW][4];
+  float4 wr[TPW][NQ];
   // the prox anchor (the client's start) is not kept in registers -- 32 more VGPRs per lane
   // spilled every prox variant -- but re-read in the update: W_start (parallel clients: one
   // [C][ld] model shared by every group, L2-resident) or the previous chained client's result,
@@ -219,21 +299,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   const float* anc = P.W_start;
   // (the weight addresses are rebuilt behind an empty asm at every use: they are used only at
   // client boundaries and must not be hoisted into registers that live across the step loop)
+  // register q of tile Tl: W + wbase() + woff(Tl, q) (16x16x4: class l16, columns 16 q + 4 lg;
+  // mb: class 4 q + mi, columns 16 mq + 4 lg), live where wok(Tl, q)
   auto wbase = [&]() {
-    int64_t b = (int64_t)l16 * ld + 64 * t0 + 4 * lg;
+    int64_t b = MB ? (int64_t)mi * ld + 64 * t0 + 16 * mq + 4 * lg : (int64_t)l16 * ld + 64 * t0 + 4 * lg;
     asm volatile("" : "+v"(b));
     return b;
   };
+  auto woff = [&](int Tl, int q) -> int64_t { return MB ? 4 * q * ld + 64 * Tl : 64 * Tl + 16 * q; };
+  auto wok = [&](int Tl, int q) { return Tl < NTS && (MB ? 4 * q + mi < C : l16 < C); };
   auto load_start = [&]() {
     const int64_t base = wbase();
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int Tl = w + NW * i;
-      const bool ok = Tl < NTS && l16 < C;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        wr[i][q] = ok ? ld4(start + base + 64 * Tl + 16 * q) : zero4;
+      for (int q = 0; q < NQ; ++q) {
+        wr[i][q] = wok(Tl, q) ? ld4(start + base + woff(Tl, q)) : zero4;
         s = sq4_acc(s, wr[i][q].x, wr[i][q].y, wr[i][q].z, wr[i][q].w);
       }
     }
@@ -244,9 +327,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int Tl = w + NW * i;
-      if (Tl < NTS && l16 < C)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st4(Wj + base + 64 * Tl + 16 * q, wr[i][q]);
+      for (int q = 0; q < NQ; ++q)
+        if (wok(Tl, q)) st4(Wj + base + woff(Tl, q), wr[i][q]);
     }
   };
   const float nw0 = load_start();                // ||W_start||^2 partial of this wave
@@ -315,10 +398,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
           const int Tl = w + NW * i;
-          if (Tl < NTS && l16 < C)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int64_t off = base + 64 * Tl + 16 * q;
+          for (int q = 0; q < NQ; ++q)
+            if (wok(Tl, q)) {
+              const int64_t off = base + woff(Tl, q);
               st4(Wj + off, ld4(start + off));
             }
         }
@@ -340,22 +423,35 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #endif
   // the forward partial z_g = X_slice W_slice^T, tile by tile, into acc (RT row tiles)
   floatx4 acc[RT];
+  floatx4 accm[RT][MB ? MBK : 1];                  // (mb) per row tile and class block
   auto fwd_tile = [&](int i) {
-    if (w + NW * i < NTS)
+    if (w + NW * i < NTS) {
+      if constexpr (MB) {
+        mb_fwd_q<0>(accm, xf[i], wr[i]);
+        mb_fwd_q<1>(accm, xf[i], wr[i]);
+        mb_fwd_q<2>(accm, xf[i], wr[i]);
+        mb_fwd_q<3>(accm, xf[i], wr[i]);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 xa[RT];
+        for (int q = 0; q < 4; ++q) {
+          float4 xa[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) xa[rt] = xf[i][rt][q];
+          for (int rt = 0; rt < RT; ++rt) xa[rt] = xf[i][rt][q];
 #pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4)
+          for (int e4 = 0; e4 < 4; ++e4)
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xa[rt], e4), comp(wr[i][q], e4), acc[rt]);
+            for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma4(comp(xa[rt], e4), comp(wr[i][q], e4), acc[rt]);
+        }
       }
+    }
   };
   auto fwd_tile0 = [&]() {
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int rt = 0; rt < RT; ++rt) {
+      acc[rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cb = 0; cb < (MB ? MBK : 1); ++cb) accm[rt][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
     fwd_tile(0);
   };
   // pre: the step's tile-0 forward ran at the end of the previous step (round 5, session 2).  A
@@ -419,7 +515,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       if (w + NW * i < NTS)                                                          \
         _Pragma("unroll") for (int rt = 0; rt < RT; ++rt)                            \
           _Pragma("unroll") for (int q = 0; q < 4; ++q)                              \
-            st4(xs_lds + img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg), xf[i][rt][q]); \
+            st4(xs_lds + (MB ? (rt * 16 + l16) * RS + 64 * (w + NW * i) + 16 * lg + 4 * q \
+                             : img_off(rt * 16 + l16, RS, w + NW * i, 4 * q + lg)),   \
+                xf[i][rt][q]);                                                       \
   }
 
       // ---------------- forward partial: z_g = X_slice W_slice^T ----------------
@@ -427,9 +525,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       if (!pre) fwd_tile0();
 #pragma unroll
       for (int i = 1; i < TPW; ++i) fwd_tile(i);
+      if constexpr (MB) {
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-        st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int cb = 0; cb < MBK; ++cb)
+            zpart[w][((rt * MBK + cb) * 4 + mb_perm(lg)) * 16 + l16] = mb_kgroup_sum(accm[rt][cb]);
+      } else {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+          st4(&zpart[w][rt * 256 + lg * 64 + l16 * 4], make_float4(acc[rt][0], acc[rt][1], acc[rt][2], acc[rt][3]));
+      }
       SP_STAMP(1)
       team_sync();  // S1: wave partials, norm partials of the previous update; the image is free
       SP_STAMP(2)
@@ -452,8 +558,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
           float v = 0.f;
           if (idx < NV - 2) {
             const int r = idx / C, c = idx - r * C;
+            const int zo = MB ? zp_off_mb<MB ? MBK : 1>(r, c) : zp_off(r, c);
 #pragma unroll
-            for (int i = 0; i < NW; ++i) v += zpart[i][zp_off(r, c)];
+            for (int i = 0; i < NW; ++i) v += zpart[i][zo];
           } else if (idx < NV) {
 #pragma unroll
             for (int i = 0; i < NW; ++i) v += wred[i][idx - (NV - 2)];
@@ -548,13 +655,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       // so the update waits only for it (the late form re-reads it per tile inside the backward,
       // behind that tile's predecessors' row loads); lanes of padding classes read class C - 1's
       // row -- every load unconditional, as the rows
-      float4 avall[PROX && NE > 0 ? TPW : 1][4];
+      float4 avall[PROX && NE > 0 ? TPW : 1][NQ];
       if constexpr (PROX && NE > 0) {
-        const float* ap = anc + (int64_t)min(l16, C - 1) * ld + 64 * t0 + 4 * lg;
+        if constexpr (MB) {
+          const float* ap = anc + 64 * t0 + 16 * mq + 4 * lg;
 #pragma unroll
-        for (int i = 0; i < TPW; ++i)
+          for (int i = 0; i < TPW; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) avall[i][q] = ld4(ap + 64 * (w + NW * i) + 16 * q);
+            for (int q = 0; q < NQ; ++q) avall[i][q] = ld4(ap + (int64_t)min(4 * q + mi, C - 1) * ld + 64 * (w + NW * i));
+        } else {
+          const float* ap = anc + (int64_t)min(l16, C - 1) * ld + 64 * t0 + 4 * lg;
+#pragma unroll
+          for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) avall[i][q] = ld4(ap + 64 * (w + NW * i) + 16 * q);
+        }
       }
       if constexpr (NE > 0)
 #pragma unroll
@@ -610,9 +725,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       // ---------------- backward + update of the register-resident slice ----------------
       // A operand lane (l16, lg): image row 4 kk + lg, block 4 (l16 & 3) + (l16 >> 2), so the
       // output register q of lane (c, lg) is the gradient of d = 16 q + 4 lg + e (the lane's W).
-      float gB[4 * RT];
+      float gB[MB ? 1 : 4 * RT];
+      if constexpr (!MB)
 #pragma unroll
-      for (int kk = 0; kk < 4 * RT; ++kk) gB[kk] = gbuf[4 * kk + lg][l16];
+        for (int kk = 0; kk < 4 * RT; ++kk) gB[kk] = gbuf[4 * kk + lg][l16];
       const float sp = (P.prox && pn2 > 0.f) ? P.mu / sqrtf(pn2) : 0.f;
       const float sr = (P.reg && wn2 > 0.f) ? P.lam / sqrtf(wn2) : 0.f;
       const float lr = P.lr;
@@ -625,6 +741,109 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       // 1), so no tile guard splits the block either
       auto bwd = [&](auto LD, auto FULL, auto EA) {
         constexpr int EAN = decltype(EA)::value;   // row loads already issued (early)
+      if constexpr (MB) {
+        // (mb) rows outer, tiles inner: one g register per batch row serves every tile and
+        // class block (lane 16 s + 4 x + j = g[r][4 s + j], broadcast from group cb by blgp);
+        // one image read per (row, tile).  The mb image is in lane order (word 16 lg + 4 q + e of
+        // a row's tile = column 16 q + 4 lg + e: the write's float4 of (row, q) lands at 16 lg + 4 q),
+        // so the read is the lane's own word of the row -- one address register, the row and tile
+        // as immediate offsets; both conflict-free (row stride = 8 mod 64 words)
+        constexpr int RS_FULL = NW * TPW * 64 + 8;
+        const int RSx = decltype(FULL)::value ? RS_FULL : RS;
+        float4 av[TPW][NQ];                         // prox anchor (late form: read per tile here)
+        if constexpr (PROX && EAN > 0) {
+#pragma unroll
+          for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) av[i][q] = avall[i][q];
+        } else if constexpr (PROX) {
+#pragma unroll
+          for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              const int Tl = w + NW * i;
+              av[i][q] = wok(Tl, q) ? ld4(anc + wbase() + woff(Tl, q)) : zero4;
+            }
+        }
+        floatx4 gm[TPW][NQ];
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) gm[i][q] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (decltype(FULL)::value && SP_MB_BWD_PF > 0) {
+          // every row block's image and g words read one block ahead, in registers
+          float xa[2][4][TPW], gq[2][4];
+          auto rd = [&](int kk, int b) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              gq[b][rr] = gbuf[4 * kk + rr][4 * lg + mi];
+#pragma unroll
+              for (int i = 0; i < TPW; ++i) xa[b][rr][i] = xs_lds[(4 * kk + rr) * RSx + 64 * (w + NW * i) + lane];
+            }
+          };
+          rd(0, 0);
+#pragma unroll
+          for (int kk = 0; kk < 4 * RT; ++kk) {
+            if (kk + 1 < 4 * RT) rd(kk + 1, (kk + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+              for (int i = 0; i < TPW; ++i) mb_bwd_row<MBK>(gm[i], xa[kk & 1][rr][i], gq[kk & 1][rr]);
+            if constexpr (decltype(LD)::value) {
+#pragma unroll
+              for (int i = 0; i < TPW; ++i) {
+                const int f = kk * TPW + i + EAN;
+                if (f < NLD) issue_row(f);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else
+#pragma unroll
+        for (int kk = 0; kk < 4 * RT; ++kk) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int r = 4 * kk + rr;
+            const float gv = gbuf[r][4 * lg + mi];
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+              const int Tl = w + NW * i;
+              if (decltype(FULL)::value || Tl < NTS)
+                mb_bwd_row<MBK>(gm[i], xs_lds[r * RSx + 64 * Tl + lane], gv);
+            }
+          }
+          if constexpr (decltype(LD)::value) {
+            // iteration (kk, i) issues load kk * TPW + i + EAN (as the 16x16x4 form: one per iteration)
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+              const int f = kk * TPW + i + EAN;
+              if (f < NLD && (decltype(FULL)::value || w + NW * (f / (4 * RT)) < NTS)) issue_row(f);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+          const int Tl = w + NW * i;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q)
+            if ((decltype(FULL)::value || Tl < NTS) && 4 * q + mi < C) {
+              float o[4];
+#pragma unroll
+              for (int e4 = 0; e4 < 4; ++e4) {
+                const float wc = comp(wr[i][q], e4);
+                const float ac = PROX ? comp(av[i][q], e4) : 0.f;
+                o[e4] = sgd_w(wc, gm[i][q][e4], lr, PROX, ac, sp, P.reg, sr);
+                if (PROX) {
+                  const float dp = o[e4] - ac;
+                  npn = sq_acc(npn, dp);
+                  nwn = sq_acc(nwn, o[e4]);
+                }
+              }
+              wr[i][q] = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         const int Tl = w + NW * i;
@@ -692,6 +911,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
           }
         }
       }
+      }
       };
       using E0 = std::integral_constant<int, 0>;
       if constexpr (NE > 0) {
@@ -720,7 +940,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
+          for (int q = 0; q < NQ; ++q)
 #pragma unroll
             for (int e4 = 0; e4 < 4; ++e4) nwn = sq_acc(nwn, comp(wr[i][q], e4));
       }
@@ -731,7 +951,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       }
       // the next step's tile-0 forward, where the next step continues this client (the weights
       // stay; a new parallel client restarts from W_start at the step's top)
-      pre = TEAMS == 1 && TPW > 1 && st + 1 < cc.steps;
+      // (mb: where the next step's forward accumulators fit beside the step's registers -- with more
+      // class blocks or partners they spilled, and a spill reload waits vmcnt(0) for the row stream:
+      // config 5 5.99 ms per launch with it, 4.70 without, profiles/r06/mb_ab.txt)
+      constexpr bool PRE_OK = !MB || (SP_MB_PRE && ((MBK <= 2 && G <= 8) || (MBK == 3 && G == 2 && !PROX)));
+      pre = TEAMS == 1 && TPW > 1 && PRE_OK && st + 1 < cc.steps;
       if (pre) fwd_tile0();
       SP_STAMP(8)
     }
@@ -754,6 +978,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
 #endif
 }
 
+#ifndef FS_SPLIT_KERNEL_ONLY   // (scripts/split_asm.sh: one instance's code, without the launchers)
 unsigned exchange_generation(const void* ws, bool long_launch) {
   static std::mutex gm;
   static std::unordered_map<const void*, unsigned> gens;
@@ -838,14 +1063,44 @@ static unsigned split_spin_limit() {
 }
 unsigned split_spin_bound() { return split_spin_limit(); }
 
-template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
-static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW, int MBK = 0>
+static void launch_split_k(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK>),
+        reinterpret_cast<const void*>(&local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, MBK>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK>), dim3(grid), dim3(WAVES * 64),
-                     lds, st, P, X);
+  hipLaunchKernelGGL((local_train_split_kernel<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, MBK>), dim3(grid),
+                     dim3(WAVES * 64), lds, st, P, X);
+}
+
+// class blocks of the mb instances for this launch (0: the 16x16x4 instances).  fs_tuning.split_mb:
+// 1 = wherever they fit (16 < B <= 32, one team), 0 = by shape, -1 = never.  By shape: C <= 8 (at
+// most 2 class blocks: half the 16x16x4 MFMA cycles or less) -- config 3 (C = 7, FedProx, G = 4)
+// 4.57 -> 4.17-4.21 ms per launch, config 1 (C = 2, narrow chained) 7.12 -> 6.44-6.53 ms; at C = 10
+// (3 blocks, 3/4 of the cycles) a tie with the read-ahead (config 2 287-290 vs 282-287 us, config 5
+// 4.70 vs 4.67 ms), so the 16x16x4 instances stay there (profiles/r06/mb_ab.txt)
+static int split_mbk(const LTParams& P, int teams) {
+  const int t = tuning().split_mb;
+  if (t < 0 || teams != 1 || split_rt(P.B) != 2) return 0;
+  const int cb = (P.C + 3) / 4;
+  if (t == 0 && cb > 2) return 0;
+  return cb;
+}
+
+// the split form's instance for this launch: the 16x16x4 one, or the mb one with ceil(C / 4)
+// class blocks (recorded for fs_local_train_last_kernel)
+template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
+static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
+  if constexpr (RT == 2 && TEAMS == 1) {
+    switch (split_mbk(P, TEAMS)) {
+      case 1: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 1>(P, X, grid, lds, st); return;
+      case 2: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 2>(P, X, grid, lds, st); return;
+      case 3: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 3>(P, X, grid, lds, st); return;
+      case 4: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 4>(P, X, grid, lds, st); return;
+      default: break;
+    }
+  }
+  launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 0>(P, X, grid, lds, st);
 }
 
 // the narrow chained instances (one tile per wave, full slices, every row load early): NT = 4 G
@@ -1121,3 +1376,6 @@ extern "C" int fs_local_train_plan(int N, int C, int B, int E, int64_t ld, int64
   *ws_bytes_out = split_ws_bytes(N, G, B, chained, cus);
   return FS_OK;
 }
+#else
+}  // namespace fs
+#endif

@@ -9,7 +9,7 @@ SRC=$1; OUT=$2; shift 2
 make -s -C $PKG/csrc
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -munsafe-fp-atomics"
 base=$(basename $SRC .hip)
-$H "$@" -c $PKG/csrc/$SRC -o $PKG/csrc/build/variant_$base.o
+$H "$@" -c $PKG/csrc/$SRC -o $PKG/csrc/build/variant_${OUT}_$base.o
 objs=$(ls $PKG/csrc/build/*.o | grep -v -e "/$base.o" -e variant_ -e _stamps -e _probe)
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $PKG/$OUT.so $objs $PKG/csrc/build/variant_$base.o -lpthread
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $PKG/$OUT.so $objs $PKG/csrc/build/variant_${OUT}_$base.o -lpthread
 echo built $PKG/$OUT.so

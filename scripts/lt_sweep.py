@@ -40,9 +40,12 @@ def main():
     ap.add_argument('--early', choices=['auto', 'off'], default='auto', help="fs_tuning.split_early (the split form's early row issue)")
     ap.add_argument('--dbuf', choices=['auto', 'on', 'off'], default='auto',
                     help="fs_tuning.split_dbuf (the split form's double-buffered instance, round 6)")
+    ap.add_argument('--mb', choices=['auto', 'on', 'off'], default='auto',
+                    help="fs_tuning.split_mb (the split form's 4x4x1 multi-block MFMA instances, round 6)")
     a = ap.parse_args()
     fedamw_amd._lib.set_tuning(split_early={'auto': 0, 'off': -1}[a.early],
-                               split_dbuf={'auto': 0, 'on': 1, 'off': -1}[a.dbuf])
+                               split_dbuf={'auto': 0, 'on': 1, 'off': -1}[a.dbuf],
+                               split_mb={'auto': 0, 'on': 1, 'off': -1}[a.mb])
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
     dev = torch.device('cuda')

@@ -35,9 +35,12 @@ def main():
     ap.add_argument('--prox', action='store_true', help="FedProx's prox term (mu = 1e-3), ridge off")
     ap.add_argument('--dbuf', choices=['auto', 'on', 'off'], default='auto',
                     help="fs_tuning.split_dbuf: the split form's double-buffered instance (round 6)")
+    ap.add_argument('--mb', choices=['auto', 'on', 'off'], default='auto',
+                    help="fs_tuning.split_mb: the split form's 4x4x1 multi-block MFMA instances (round 6)")
     a = ap.parse_args()
     assert os.environ.get('FEDSIM_LIB', '').endswith('stamps.so'), 'run with FEDSIM_LIB=.../libfedsim_stamps.so'
-    fedamw_amd._lib.set_tuning(split_dbuf={'auto': 0, 'on': 1, 'off': -1}[a.dbuf])
+    fedamw_amd._lib.set_tuning(split_dbuf={'auto': 0, 'on': 1, 'off': -1}[a.dbuf],
+                               split_mb={'auto': 0, 'on': 1, 'off': -1}[a.mb])
     sh = SHAPES[a.config]
     chained = a.chained or sh.get('chained', False)
     dev = torch.device('cuda')

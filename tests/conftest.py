@@ -26,3 +26,14 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if 'gpu' in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def mb_off():
+    """The split form's 16x16x4 instances for the whole test (fs_tuning.split_mb = -1): the modules
+    that hold the pair, pipe, team and double-buffered forms BITWISE to the split form compare
+    within that family -- the mb instances (4x4x1 MFMAs, another summation order) are held to the
+    oracle in test_gpu_mb.py."""
+    from fedamw_amd import _lib
+    with _lib.tuning(split_mb=-1):
+        yield

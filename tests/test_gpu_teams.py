@@ -14,7 +14,7 @@ import torch
 from oracle import fedsim_oracle as O
 from tests.test_gpu_parity import _rand_clients, _train_via_abi, amd  # noqa: F401 (fixture)
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("mb_off")]
 
 
 def _teams(amd, G):
