@@ -129,9 +129,14 @@ __device__ __forceinline__ float mb_kgroup_sum(floatx4 a) {
   return s01 + s23;
 }
 __device__ __forceinline__ int mb_perm(int lg) { return ((lg & 1) << 1) | (lg >> 1); }
-// offset of (row, class) in a wave's mb partial-logit block [rt][class block][j][l16]
+// offset of (row, class) in a wave's mb partial-logit block [rt][class block][j][l16 ^ 4 cb]: the
+// rows of a 16-word segment XOR-swizzled by the class block, so the hand-off's (row, class) reads
+// (classes c, c + 4, c + 8 of one row: the same j) fall in different banks; the writes (one
+// segment per 16-lane group) stay a permutation of the block's 64 words
 template <int CB>
-__device__ __forceinline__ int zp_off_mb(int r, int c) { return ((r >> 4) * CB + (c >> 2)) * 64 + (c & 3) * 16 + (r & 15); }
+__device__ __forceinline__ int zp_off_mb(int r, int c) {
+  return ((r >> 4) * CB + (c >> 2)) * 64 + (c & 3) * 16 + ((r & 15) ^ ((c >> 2) << 2));
+}
 
 // Per-lane d mapping inside a 64-column tile (forward operand, weights, gradient):
 // lane (l16, lg), register q, component e  <->  d = 16 q + 4 lg + e.  One load instruction
@@ -530,7 +535,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int cb = 0; cb < MBK; ++cb)
-            zpart[w][((rt * MBK + cb) * 4 + mb_perm(lg)) * 16 + l16] = mb_kgroup_sum(accm[rt][cb]);
+            zpart[w][((rt * MBK + cb) * 4 + mb_perm(lg)) * 16 + (l16 ^ (cb << 2))] = mb_kgroup_sum(accm[rt][cb]);
       } else {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
@@ -776,9 +781,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
           auto rd = [&](int kk, int b) {
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
+#ifdef SP_MB_DIAG_NOGREAD   // diagnostic builds only (wrong results): which LDS reads the backward waits for
+              gq[b][rr] = gbuf[0][4 * lg + mi] + (float)(kk + rr);
+#else
               gq[b][rr] = gbuf[4 * kk + rr][4 * lg + mi];
+#endif
 #pragma unroll
-              for (int i = 0; i < TPW; ++i) xa[b][rr][i] = xs_lds[(4 * kk + rr) * RSx + 64 * (w + NW * i) + lane];
+              for (int i = 0; i < TPW; ++i)
+#ifdef SP_MB_DIAG_NOXREAD
+                xa[b][rr][i] = (float)(kk * 4 + rr + i) * gq[b][rr];
+#else
+                xa[b][rr][i] = xs_lds[(4 * kk + rr) * RSx + 64 * (w + NW * i) + lane];
+#endif
             }
           };
           rd(0, 0);
@@ -1076,14 +1090,15 @@ static void launch_split_k(const LTParams& P, const SplitWS& X, int grid, size_t
 // class blocks of the mb instances for this launch (0: the 16x16x4 instances).  fs_tuning.split_mb:
 // 1 = wherever they fit (16 < B <= 32, one team), 0 = by shape, -1 = never.  By shape: C <= 8 (at
 // most 2 class blocks: half the 16x16x4 MFMA cycles or less) -- config 3 (C = 7, FedProx, G = 4)
-// 4.57 -> 4.17-4.21 ms per launch, config 1 (C = 2, narrow chained) 7.12 -> 6.44-6.53 ms; at C = 10
-// (3 blocks, 3/4 of the cycles) a tie with the read-ahead (config 2 287-290 vs 282-287 us, config 5
-// 4.70 vs 4.67 ms), so the 16x16x4 instances stay there (profiles/r06/mb_ab.txt)
-static int split_mbk(const LTParams& P, int teams) {
+// 4.57 -> 4.07-4.08 ms per launch, config 1 (C = 2, narrow chained) 7.07 -> 6.09-6.11 ms -- and
+// 3 blocks at G = 16 (config 5: 4.66-4.68 -> 4.51-4.55 ms); at G = 2 (config 2) 283-285 vs 288-290 us:
+// that step waits for its row stream, not for its MFMAs (without the backward's LDS reads the mb
+// launch measured the same, profiles/r06/mb_ab.txt), so the 16x16x4 instances stay there
+static int split_mbk(const LTParams& P, int G, int teams) {
   const int t = tuning().split_mb;
   if (t < 0 || teams != 1 || split_rt(P.B) != 2) return 0;
   const int cb = (P.C + 3) / 4;
-  if (t == 0 && cb > 2) return 0;
+  if (t == 0 && cb > 2 && !(cb == 3 && G >= 16)) return 0;
   return cb;
 }
 
@@ -1092,7 +1107,7 @@ static int split_mbk(const LTParams& P, int teams) {
 template <int RT, int G, bool PROX, int EARLY, int TEAMS, int WAVES = SP_WAVES, int TPWK = SP_TPW>
 static void launch_split_s(const LTParams& P, const SplitWS& X, int grid, size_t lds, hipStream_t st) {
   if constexpr (RT == 2 && TEAMS == 1) {
-    switch (split_mbk(P, TEAMS)) {
+    switch (split_mbk(P, G, TEAMS)) {
       case 1: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 1>(P, X, grid, lds, st); return;
       case 2: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 2>(P, X, grid, lds, st); return;
       case 3: set_last_lt_kernel(FS_LT_MB); launch_split_k<RT, G, PROX, EARLY, TEAMS, WAVES, TPWK, 3>(P, X, grid, lds, st); return;

@@ -133,7 +133,7 @@ def test_mb_timeout_raises(amd):
 
 def test_mb_selection(amd):
     """Which launches take the mb instances: by shape (split_mb = 0) where C <= 8 (at most 2
-    class blocks: configs 1 and 3), split_mb = 1 wherever the split form runs with 16 < B <= 32;
+    class blocks: configs 1 and 3) or C <= 12 at G = 16 (config 5), split_mb = 1 wherever the split form runs with 16 < B <= 32;
     B <= 16 (one row tile) stays on the 16x16x4 instances; -1 never."""
     rs = np.random.RandomState(8)
 
@@ -144,7 +144,8 @@ def test_mb_selection(amd):
             _train_via_abi(amd, Xs, ys, W0, 0.3, 2, B, False, 0.0, False, 0.0, chained, split=G)
             return amd.lib.LT_KERNELS[amd.lib.lib().fs_local_train_last_kernel()]
 
-    assert kernel(2048, 32, 2) == 'split'                  # C = 10 by shape: the 16x16x4 instances
+    assert kernel(2048, 32, 2) == 'split'                  # C = 10 at G = 2 by shape: the 16x16x4 instances
+    assert kernel(16384, 32, 16) == 'mb'                   # C = 10 at G = 16 (config 5's shape class)
     assert kernel(2048, 32, 2, C=8) == 'mb'                # C <= 8 by shape
     assert kernel(4096, 32, 4, C=7) == 'mb'                # config 3's shape class
     assert kernel(2000, 32, 8, chained=True, C=2) == 'mb'  # config 1's (narrow chained)
