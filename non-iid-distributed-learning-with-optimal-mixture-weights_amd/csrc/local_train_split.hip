@@ -190,11 +190,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   static_assert(MBK >= 0 && MBK <= 4 && (MBK == 0 || TEAMS == 1), "mb");
   constexpr bool MB = MBK > 0;
   constexpr int NQ = MB ? MBK : 4;                 // weight registers per tile: q (16x16x4) or class block (mb)
+  constexpr int NCS = !MB || MBK > 2 ? 16 : 4 * MBK; // softmax lanes per row (a power of 2 >= the padded classes)
   constexpr int NW = WAVES / TEAMS;                // waves per client lane
   constexpr int NTH = NW * 64;
   constexpr int NC = 16;
   constexpr int NR = RT * 16;
   constexpr int NZ = NR * NC;
+  constexpr int NZS = NR * NCS;
   constexpr int TPW = TPWK;
   constexpr int XT = NTH;                         // threads running the hand-off
   // exchanged values per hand-off thread: NR*C logits + 2 norms (G >= 8: NR*C + 2 <= 512)
@@ -230,6 +232,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   const int NT = (int)(ld >> 6);
   const int C = P.C, B = P.B, E = P.E;
   const int NV = NR * C + 2;
+  static_assert(NZS % 64 == 0, "the softmax loop must stay wave-uniform");
 
   // block -> (group, slice).  Chained: 8*G blocks are launched and those with
   // blockIdx % 8 == 0 take part (one XCD under round-robin placement).  Parallel: consecutive
@@ -387,6 +390,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
     lc_ok = sp_advance(lc, P, grp, ng, T);
     if (lc_ok) fetch_rows();
   }
+  if constexpr (NCS < NC)                         // the classes the mb softmax never writes
+    for (int i = tid; i < NR * NC; i += NTH) gbuf[i / NC][i % NC] = 0.f;
   __syncthreads();
 
   // clients with no step (n_j = 0 or E = 0): the result is the client's start -- the
@@ -500,7 +505,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       // (the narrow chained instances keep the fetch at the step's end: their step is the hand-off
       // chain, and these loads ahead of its polls cost more than the stream's tail -- config 1
       // 7.0 vs 7.6 ms per launch, profiles/r05b/prefwd_forms.txt)
-      constexpr bool TOP_FETCH = TPW > 1;
+#ifndef SP_NARROW_TOP
+#define SP_NARROW_TOP 0
+#endif
+      constexpr bool TOP_FETCH = TPW > 1 || SP_NARROW_TOP;
       auto fetch_next = [&]() {
         if (ilv) {
           if (w == 0 && lg == 0)
@@ -687,21 +695,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
       SP_STAMP(6)
       const float invb = 1.0f / (float)bc;
       float cep = 0.f;
-      for (int idx = tid; idx < NZ; idx += NTH) {          // NC lanes of one wave hold one row
-        const int r = idx / NC, c = idx - r * NC;
+      // (mb: NCS lanes per row, the class blocks' width rounded to a power of 2 -- 4 at C <= 4, 8 at
+      // C <= 8; the classes past it stay the zeros written at the kernel's start.  The same sums:
+      // the 16-lane trees only added exact zeros from lanes past NCS)
+      for (int idx = tid; idx < NZS; idx += NTH) {         // NCS lanes of one wave hold one row
+        const int r = idx / NCS, c = idx - r * NCS;
         const bool valid = r < bc && c < C;
         const float z = valid ? zsum[r][c] : 0.f;
-        // (the loop is wave-uniform -- NZ is a multiple of 64 -- so the DPP exchanges run with
+        // (the loop is wave-uniform -- NZS is a multiple of 64 -- so the DPP exchanges run with
         // every lane active)
         float m = valid ? z : -INFINITY;
 #pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
+        for (int off = NCS / 2; off > 0; off >>= 1) m = fmaxf(m, xor_get(m, off, lane));
         // softmax on v_exp_f32 / v_rcp_f32 / v_log_f32 (one exponential per entry, e / sum e
         // for the gradient): within the fp32 tolerance of torch's log_softmax (tests/fixtures.py)
         const float ex = valid ? __expf(z - m) : 0.f;
         float se = ex;
 #pragma unroll
-        for (int off = NC / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
+        for (int off = NCS / 2; off > 0; off >>= 1) se += xor_get(se, off, lane);
         float gv = 0.f;
         if (valid) {
           const bool isy = c == lab[par][r];
