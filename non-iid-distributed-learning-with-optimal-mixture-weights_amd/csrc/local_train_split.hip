@@ -1192,7 +1192,10 @@ static void launch_split_g(const LTParams& P, const SplitWS& X, int grid, size_t
   // late 5,102-5,107; early 1: 4,678-4,691, 2: 4,488-4,530, 3: 4,605-4,622, 4: 4,539-4,544, 6: 4,699-4,715,
   // 8: 4,713-4,720)
   constexpr int EARLY_G = (G == 2 && SP_EARLY > 4) ? 4 : SP_EARLY;
-  constexpr int EARLY_PROX = SP_EARLY < 2 ? SP_EARLY : 2;
+#ifndef SP_EP
+#define SP_EP 2
+#endif
+  constexpr int EARLY_PROX = SP_EARLY < SP_EP ? SP_EARLY : SP_EP;
   const bool full = (P.ld >> 6) == (int64_t)G * SP_WAVES * SP_TPW;
   const bool early = full && EARLY_G > 0 && tuning().split_early >= 0;
   if (launch_split_narrow<RT, G>(P, X, grid, lds, st)) return;
