@@ -156,3 +156,40 @@ def test_bench_two_ranks_launcher():
     assert line['dist']['world_size'] == 2 and line['dist']['backend'] == 'gloo'
     assert line['dist']['allreduce_check'] == 3.0
     assert line['value'] > 0 and line['config']['clients_total'] == 200
+
+
+def _worker_rccl(rank, world, port, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      HSA_ENABLE_IPC_MODE_LEGACY='0')
+    torch.cuda.set_device(rank)
+    torch.distributed.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', rank))
+    try:
+        dev = torch.device('cuda', rank)
+        # the per-round all-reduce of the partial aggregate (C x ld at config 2) and the Z
+        # all-gather into rank blocks, through RCCL with one rank
+        g = torch.Generator(device='cpu').manual_seed(9)
+        W = torch.randn(10, 2048, generator=g).to(dev)
+        ref = W.clone()
+        torch.distributed.all_reduce(W, op=torch.distributed.ReduceOp.SUM)
+        Z = torch.randn(64, 40, generator=g).to(dev)
+        Zo = torch.empty(64 * 40, device=dev)
+        torch.distributed.all_gather_into_tensor(Zo, Z.contiguous().view(-1))
+        torch.cuda.synchronize()
+        out[rank] = (torch.equal(W, ref), torch.equal(Zo.view(64, 40), Z),
+                     torch.distributed.get_backend())
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_rccl_world_one_collectives():
+    """The RCCL path itself on the box's one GPU: a one-rank ``nccl`` process group (RCCL on
+    ROCm) runs the two collectives the sharded round issues -- the all-reduce of the partial
+    aggregate (dist.allreduce_sum_) and the all-gather of Z into rank blocks
+    (dist.allgather_z, blocked) -- and returns the input unchanged.  Two ranks need two GPUs
+    (RCCL refuses a shared device); the 8-GPU run is the driver's."""
+    mgr = mp.get_context('spawn').Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_rccl, args=(1, _free_port(), out), nprocs=1, join=True)
+    ok_ar, ok_ag, backend = out[0]
+    assert backend == 'nccl'
+    assert ok_ar and ok_ag
