@@ -62,6 +62,9 @@ constexpr int SP_EARLY = SP_E1 + SP_E2 + SP_E3;
 // it the reads waited just in time: config 2 313 -> 288 us per launch, config 5 5.99 -> 5.58 ms,
 // profiles/r06/mb_ab.txt), and the next step's tile-0 forward at the step's end (SP_MB_PRE, where
 // it fits: PRE_OK in the kernel)
+#ifndef SP_MB_RSP
+#define SP_MB_RSP 4   // (the mb image's row stride mod 32, RSP in the kernel; 8 = round 6's first form, for A/B)
+#endif
 #ifndef SP_MB_BWD_PF
 #define SP_MB_BWD_PF 1
 #endif
@@ -263,7 +266,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
   const int T = P.chained ? P.N : (P.N + ng - 1) / ng;     // client sequence length
   const int t0 = tile_lo(g, G, NT), t1 = tile_lo(g + 1, G, NT);
   const int NTS = t1 - t0;                       // tiles of this slice
-  const int RS = NTS * 64 + 8;                   // LDS row stride (floats)
+  // LDS row stride (floats): 8 mod 64 for the 16x16x4 image (its swizzle assumes it); 4 mod 32 for
+  // the mb image, whose ds_write_b128 of 8 consecutive rows (one 8-lane group) then covers the 32
+  // banks once -- at 8 mod 32 rows r and r + 4 shared banks: 2-way, and 29-30 % of the mb
+  // instances' LDS-array cycles were bank conflicts (profiles/r06/pmc_c3.txt, pmc_c5.txt)
+  constexpr int RSP = MB ? SP_MB_RSP : 8;
+  const int RS = NTS * 64 + RSP;
   // this lane's slice image; an expression, not a pointer variable: through a local pointer
   // hipcc lost the image's distinctness from the static LDS arrays and waited lgkmcnt(0) in
   // three places of the step (config 5: 5.28 -> 6.09 ms per launch, profiles/r04/teams_split_regression.txt);
@@ -763,8 +771,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void local_train_split_kernel(LTPara
         // one image read per (row, tile).  The mb image is in lane order (word 16 lg + 4 q + e of
         // a row's tile = column 16 q + 4 lg + e: the write's float4 of (row, q) lands at 16 lg + 4 q),
         // so the read is the lane's own word of the row -- one address register, the row and tile
-        // as immediate offsets; both conflict-free (row stride = 8 mod 64 words)
-        constexpr int RS_FULL = NW * TPW * 64 + 8;
+        // as immediate offsets; both conflict-free (row stride = 4 mod 32 words, RSP)
+        constexpr int RS_FULL = NW * TPW * 64 + RSP;
         const int RSx = decltype(FULL)::value ? RS_FULL : RS;
         float4 av[TPW][NQ];                         // prox anchor (late form: read per tile here)
         if constexpr (PROX && EAN > 0) {
