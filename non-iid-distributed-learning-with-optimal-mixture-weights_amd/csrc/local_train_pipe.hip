@@ -48,7 +48,7 @@ constexpr int PP_NTS = PP_WAVES * PP_TPW;
 constexpr int PP_RS = PP_NTS * 64 + 8;    // LDS image row stride (floats)
 constexpr int PP_NR = 32;                 // batch rows (two 16-row tiles)
 constexpr int PP_SZ = 520;                // granules per (group, parity, slice): [rt][kk][lane] + 2 norms
-constexpr int PP_ZS = 20;                 // transposed partial-logit block: floats per class (16 + pad)
+constexpr int PP_ZS = 16;                 // transposed partial-logit block: floats per class
 constexpr int PP_ERR_BYTES = 256;
 
 // In-loop loads are inline asm (tagged as the pair form's: `; pr-row`, `; pr-idx`, `; pr-poll`),
@@ -112,8 +112,12 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
   static_assert(NRM || !PROX, "the prox term exchanges the norms");
   constexpr int NW = PP_WAVES, TPW = PP_TPW, RS = PP_RS, NC = 16;
   constexpr int GP = G > 1 ? G - 1 : 1;          // partners
-  // wave partial logits, transposed: zpt[w][rt][class * ZS + 4 lg + kk] = the partial of row
-  // 16 rt + 4 kk + lg -- one ds_read_b128 per wave gives a lane its four rows of the tile
+  // wave partial logits, transposed: zpt[w][rt][class * ZS + 4 (kk ^ zsw(class)) + lg] = the partial
+  // of row 16 rt + 4 lg + kk -- one ds_read_b128 per wave gives a lane its four rows of the tile.
+  // The float4 slots of a class are XOR-swizzled by (class >> 1) & 3 (round 6): at a 20-float
+  // class stride (unswizzled) the reads' 16-lane groups hit a bank twice, 22 % of the form's
+  // LDS-array cycles in conflicts at config 4 (profiles/r06/pmc_c4.txt); now the reads are
+  // conflict-free and the ds_write_b32 of the partials at most 2-way (free, MI355X_MICROARCH.md LDS)
   __shared__ __attribute__((aligned(16))) float zpt[NW][2][NC * PP_ZS];
   // softmax gradients of the step (by parity): gsm[par][rt][lane][kk] = g of (row 16 rt + 4 kk + lg,
   // class l16), written by wave 4 rt + kk, read back by every wave as one ds_read_b128; the
@@ -357,13 +361,13 @@ __global__ __launch_bounds__(PP_THREADS, 1) void local_train_pipe_kernel(LTParam
           for (int e4 = 0; e4 < 4; ++e4) a = mfma4(xf[i][rt][q][e4], wr[i][q][e4], a);
       // a[j] = partial logit of (row 16 rt + 4 lg + j, class l16)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) zpt[w][rt][l16 * PP_ZS + 4 * j + lg] = a[j];
+      for (int j = 0; j < 4; ++j) zpt[w][rt][l16 * PP_ZS + 4 * (j ^ ((l16 >> 1) & 3)) + lg] = a[j];
     };
     // ---- the own slice's partials of one tile (wave order) ----
     auto own_sum = [&](int rt) {
       float4 p[NW];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) p[i] = ld4(&zpt[i][rt][l16 * PP_ZS + 4 * lg]);
+      for (int i = 0; i < NW; ++i) p[i] = ld4(&zpt[i][rt][l16 * PP_ZS + 4 * (lg ^ ((l16 >> 1) & 3))]);
       floatx4 v = zero4;
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
