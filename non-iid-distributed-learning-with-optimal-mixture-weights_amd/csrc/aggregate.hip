@@ -108,26 +108,30 @@ __global__ __launch_bounds__(256) void aggregate_one_kernel(const float* __restr
   const int j0 = sub * per, j1 = min(N, j0 + per);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < len4 && j0 < j1) {
+    // every load of a group of 8 clients (the range's first included) issued before the first
+    // fold: one round trip per 8 clients (round 6; the first client's load, then groups of 8 / 4,
+    // then the tail one by one took 4 dependent round trips at config 2's 7 clients per range).
+    // The same products and sums in the same order as the left fold of the range.
     const float* base = W + 4 * i;
-    const float4 w0 = ld4(base + (int64_t)j0 * stride);
-    const float p0 = p[j0];
-    acc = make_float4(p0 * w0.x, p0 * w0.y, p0 * w0.z, p0 * w0.w);
-    int j = j0 + 1;
-    for (; j + 7 < j1; j += 8) {                 // 8 loads in flight per round trip
+    for (int j = j0; j < j1; j += 8) {
+      const int n = min(8, j1 - j);
       float4 v[8];
+      float pv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ld4(base + (int64_t)(j + u) * stride);
+      for (int u = 0; u < 8; ++u)
+        if (u < n) {
+          v[u] = ld4(base + (int64_t)(j + u) * stride);
+          pv[u] = p[j + u];
+        }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = fold_step(acc, p[j + u], v[u]);
+      for (int u = 0; u < 8; ++u)
+        if (u < n) {
+          if (u == 0 && j == j0)
+            acc = make_float4(pv[0] * v[0].x, pv[0] * v[0].y, pv[0] * v[0].z, pv[0] * v[0].w);
+          else
+            acc = fold_step(acc, pv[u], v[u]);
+        }
     }
-    for (; j + 3 < j1; j += 4) {
-      float4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = ld4(base + (int64_t)(j + u) * stride);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc = fold_step(acc, p[j + u], v[u]);
-    }
-    for (; j < j1; ++j) acc = fold_step(acc, p[j], ld4(base + (int64_t)j * stride));
   }
   sums[sub][pl] = acc;
   __syncthreads();
